@@ -1,0 +1,199 @@
+"""ctypes binding of libdvie.so (the C ABI declared in include/dvie.h).
+
+The structures below mirror include/dvie.h field for field; `load()` checks every
+struct size against `dvie_abi_sizeof` so a header/binding mismatch fails at import.
+The library is the only compute path: if it is missing or fails to load, every op
+raises — there is no CPU or PyTorch fallback.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; libdvie reuses it)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdvie.so")
+
+DVIE_OK = 0
+DVIE_EINVAL = 1001
+F32, BF16 = 0, 1
+ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU = 0, 1, 2, 3
+EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW = range(8)
+LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC = range(6)
+OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int
+i64 = ctypes.c_longlong
+f32 = ctypes.c_float
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", vp), ("w", vp), ("y", vp), ("bias", vp), ("res", vp), ("z", vp),
+        ("x_ld", i64), ("y_ld", i64), ("res_ld", i64), ("z_ld", i64),
+        ("n", i32), ("ih", i32), ("iw", i32), ("c", i32),
+        ("kpad", i32), ("cout", i32),
+        ("oh", i32), ("ow", i32), ("sy", i32), ("sx", i32),
+        ("th", i32), ("tw", i32), ("dy0", i32), ("dx0", i32), ("ddy", i32), ("ddx", i32),
+        ("yh", i32), ("yw", i32), ("osy", i32), ("osx", i32), ("ory", i32), ("orx", i32),
+        ("act", i32), ("dact", i32), ("beta", i32), ("dtype", i32),
+        ("out_f32", i32), ("alpha", f32),
+    ]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [
+        ("g", vp), ("x", vp), ("ws", vp),
+        ("g_ld", i64), ("x_ld", i64),
+        ("n", i32), ("oh", i32), ("ow", i32), ("cout", i32),
+        ("ih", i32), ("iw", i32), ("c", i32), ("sy", i32),
+        ("sx", i32), ("th", i32), ("tw", i32), ("dy0", i32),
+        ("dx0", i32), ("ddy", i32), ("ddx", i32), ("splits", i32),
+        ("dtype", i32), ("pad0", i32),
+    ]
+
+
+class WreduceDesc(ctypes.Structure):
+    _fields_ = [
+        ("ws", vp), ("dw", vp), ("cinv", vp),
+        ("splits", i32), ("ws_rows", i32), ("ws_k", i32), ("co_off", i32),
+        ("cout_p", i32), ("cin_p", i32), ("kh_n", i32), ("kw_n", i32),
+        ("c", i32), ("beta", i32),
+    ]
+
+
+class ColsumDesc(ctypes.Structure):
+    _fields_ = [
+        ("g", vp), ("ws", vp), ("g_ld", i64), ("rows", i64),
+        ("c", i32), ("splits", i32), ("dtype", i32), ("pad0", i32),
+    ]
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [
+        ("src", vp), ("dst", vp), ("cmap", vp),
+        ("rows", i32), ("kpad", i32), ("c", i32), ("mode", i32),
+        ("th", i32), ("tw", i32), ("kh0", i32), ("kw0", i32),
+        ("dkh", i32), ("dkw", i32), ("cout_s", i32), ("cin_s", i32),
+        ("kh_s", i32), ("kw_s", i32), ("dtype", i32), ("pad0", i32),
+    ]
+
+
+class EwDesc(ctypes.Structure):
+    _fields_ = [
+        ("y", vp), ("src0", vp), ("src1", vp), ("src2", vp), ("res", vp), ("z", vp),
+        ("ext", vp), ("mean", vp), ("std", vp),
+        ("y_ld", i64), ("src_ld0", i64), ("src_ld1", i64), ("src_ld2", i64), ("res_ld", i64), ("z_ld", i64),
+        ("sn", i64), ("sc", i64), ("sh", i64), ("sw", i64),
+        ("op", i32), ("n", i32), ("h", i32), ("w", i32),
+        ("c", i32), ("nsrc", i32), ("sh0", i32), ("sw0", i32),
+        ("sh1", i32), ("sw1", i32), ("sh2", i32), ("sw2", i32),
+        ("act", i32), ("dact", i32), ("beta", i32), ("dtype", i32),
+        ("ext_c", i32), ("pad0", i32),
+        ("alpha", f32), ("scale", f32),
+    ]
+
+
+class LossDesc(ctypes.Structure):
+    _fields_ = [
+        ("a", vp), ("b", vp), ("grad", vp), ("out", vp), ("partial", vp), ("ws", vp),
+        ("a_sn", i64), ("a_sc", i64), ("a_sh", i64), ("a_sw", i64),
+        ("b_sn", i64), ("b_sc", i64), ("b_sh", i64), ("b_sw", i64),
+        ("kind", i32), ("bsz", i32), ("ch", i32), ("h", i32),
+        ("w", i32), ("beta", i32), ("dtype", i32), ("pad0", i32),
+        ("weight", f32), ("pad1", f32),
+    ]
+
+
+class WarpDesc(ctypes.Structure):
+    _fields_ = [
+        ("img", vp), ("flow", vp), ("out", vp), ("dout", vp), ("dimg", vp), ("dflow", vp),
+        ("n", i32), ("c", i32), ("h", i32), ("w", i32),
+        ("align_corners", i32), ("pad0", i32),
+    ]
+
+
+class PackList(ctypes.Structure):
+    _fields_ = [("descs_dev", vp), ("n", i32), ("max_elems", i32)]
+
+
+class _OpUnion(ctypes.Union):
+    _fields_ = [
+        ("conv", ConvDesc), ("wgrad", WgradDesc), ("wreduce", WreduceDesc), ("colsum", ColsumDesc),
+        ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList),
+    ]
+
+
+class Op(ctypes.Structure):
+    _fields_ = [("kind", i32), ("pad0", i32), ("u", _OpUnion)]
+
+
+_ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
+        OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, 100: WarpDesc}
+
+EXPORTS = [
+    "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
+    "dvie_ew", "dvie_loss", "dvie_loss_partial_count", "dvie_loss_ws_floats", "dvie_warp_fwd",
+    "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
+    "dvie_last_error",
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+class DvieError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libdvie.so once; raise loudly if it is absent or its ABI does not match."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise DvieError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no non-HIP fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.dvie_abi_sizeof.restype = ctypes.c_size_t
+        lib.dvie_abi_sizeof.argtypes = [i32]
+        for which, st in _ABI.items():
+            got = lib.dvie_abi_sizeof(which)
+            if got != ctypes.sizeof(st):
+                raise DvieError(f"ABI mismatch for {st.__name__}: C {got} vs ctypes {ctypes.sizeof(st)}")
+        lib.dvie_version.restype = ctypes.c_char_p
+        lib.dvie_last_error.restype = ctypes.c_char_p
+        for name in ("dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_ew",
+                     "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd"):
+            getattr(lib, name).argtypes = [vp, vp]
+            getattr(lib, name).restype = i32
+        lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]
+        lib.dvie_run_ops.argtypes = [vp, i32, vp]
+        lib.dvie_loss_partial_count.argtypes = [vp]
+        lib.dvie_loss_partial_count.restype = ctypes.c_size_t
+        lib.dvie_loss_ws_floats.argtypes = [vp]
+        lib.dvie_loss_ws_floats.restype = ctypes.c_size_t
+        lib.dvie_adamax.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
+        lib.dvie_scale.argtypes = [vp, i64, f32, vp]
+        _lib = lib
+        return lib
+
+
+def check(rc, what=""):
+    if rc != DVIE_OK:
+        msg = load().dvie_last_error().decode(errors="replace") if rc == DVIE_EINVAL else f"hipError {rc}"
+        raise DvieError(f"{what}: {msg}")
+
+
+def stream_ptr(device=None):
+    """Raw hipStream_t of torch's current stream."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(t):
+    if not t.is_cuda:
+        raise DvieError("dvie ops run on the MI355X only: tensor is on %s (no CPU fallback)" % t.device)

@@ -1,0 +1,92 @@
+// Shared device helpers for the gfx950 kernels (bf16 <-> f32, 4-channel vectors,
+// activation functions and their output-side derivatives, error plumbing).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/dvie.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+typedef uint16_t bf16_t;  // raw bf16 storage
+
+namespace dvie {
+
+void set_error(const char* fmt, ...);
+
+#define DVIE_CHECK_ARG(cond, ...)      \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::dvie::set_error(__VA_ARGS__);  \
+      return DVIE_EINVAL;              \
+    }                                  \
+  } while (0)
+
+#define DVIE_RETURN_LAUNCH()                     \
+  do {                                           \
+    hipError_t _e = hipGetLastError();           \
+    return _e == hipSuccess ? DVIE_OK : (int)_e; \
+  } while (0)
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// 4-element vector access (fp32: 16 B, bf16: 8 B)
+template <typename T>
+struct V4;
+template <>
+struct V4<float> {
+  __device__ __forceinline__ static f32x4 load(const float* p) { return *(const f32x4*)p; }
+  __device__ __forceinline__ static void store(float* p, f32x4 v) { *(f32x4*)p = v; }
+};
+template <>
+struct V4<bf16_t> {
+  __device__ __forceinline__ static f32x4 load(const bf16_t* p) {
+    i32x2 r = *(const i32x2*)p;
+    f32x4 v;
+    v[0] = __uint_as_float(((uint32_t)r[0]) << 16);
+    v[1] = __uint_as_float(((uint32_t)r[0]) & 0xffff0000u);
+    v[2] = __uint_as_float(((uint32_t)r[1]) << 16);
+    v[3] = __uint_as_float(((uint32_t)r[1]) & 0xffff0000u);
+    return v;
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, f32x4 v) {
+    i32x2 r;
+    r[0] = (int)((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16));
+    r[1] = (int)((uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    *(i32x2*)p = r;
+  }
+};
+
+__device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
+  switch (act) {
+    case DVIE_ACT_LRELU: return v > 0.f ? v : v * alpha;
+    case DVIE_ACT_ELU: return v > 0.f ? v : expm1f(v);
+    case DVIE_ACT_RELU: return v > 0.f ? v : 0.f;
+    default: return v;
+  }
+}
+
+// derivative expressed through the activation OUTPUT z
+__device__ __forceinline__ float act_dz(float z, int act, float alpha) {
+  switch (act) {
+    case DVIE_ACT_LRELU: return z > 0.f ? 1.f : alpha;
+    case DVIE_ACT_ELU: return z > 0.f ? 1.f : z + 1.f;
+    case DVIE_ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+__host__ __device__ __forceinline__ int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace dvie

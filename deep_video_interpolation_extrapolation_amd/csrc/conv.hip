@@ -1,0 +1,636 @@
+// Convolution kernels for gfx950 (MI355X, CDNA4).
+//
+// conv_igemm: NHWC implicit GEMM on MFMA.  rows = output channels (the MFMA "A"
+//   operand, packed weights [cout][kpad]), columns = output pixels (the MFMA "B"
+//   operand, gathered from the NHWC input on the fly, one tap at a time).  Both operands
+//   are K-contiguous in memory, so every global load is a 16-byte vector and both LDS
+//   images use the same 128-byte rows (8 x 16 B chunks, XOR-swizzled by row).
+//   fp32 mode: v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, parity mode);
+//   bf16 mode: v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+//   Register-staged double buffer: the next K-step's global loads are issued before
+//   the MFMAs of the current one and written to the other LDS buffer after them (one
+//   barrier per K-step).
+//
+// wgrad: per tap, dW[co][ci] = sum_pix g[pix][co] * x[pix+tap][ci], split over pixel
+//   chunks into fp32 partial slabs (no atomics, deterministic), reduced by wreduce into
+//   the OIHW fp32 parameter gradient.  bf16 operands reach MFMA through
+//   ds_read_b64_tr_b16 transposed reads of [pixel][channel] LDS images.
+//
+// Reference ops replaced: nn.Conv2d forward / backward of nets/HRNet.py (all 77 convs)
+// and nets/vgg.py:11-54 (VGG19 features).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace dvie {
+
+static thread_local char g_err[512];
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+const char* last_error() { return g_err; }
+
+// ----------------------------------------------------------------------------------
+// implicit GEMM forward / data-gradient
+// ----------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void mfma_chunk(f32x4& acc, const i32x4& a, const i32x4& b);
+
+template <>
+__device__ __forceinline__ void mfma_chunk<float>(f32x4& acc, const i32x4& a, const i32x4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[0]), __int_as_float(b[0]), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[1]), __int_as_float(b[1]), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[2]), __int_as_float(b[2]), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[3]), __int_as_float(b[3]), acc, 0, 0, 0);
+}
+
+template <>
+__device__ __forceinline__ void mfma_chunk<bf16_t>(f32x4& acc, const i32x4& a, const i32x4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                acc, 0, 0, 0);
+}
+
+// byte offset of 16-byte chunk `ch` (0..7) of LDS row `row` (128-byte rows)
+__device__ __forceinline__ int swz128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+template <typename T, int BC, int BP, int WC, int WP, bool OUTF32>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(const dvie_conv_desc p) {
+  typedef typename std::conditional<OUTF32, float, T>::type OutT;
+  constexpr int ES = sizeof(T);
+  constexpr int VEC = 16 / ES;
+  constexpr int KSTEP = 128 / ES;
+  constexpr int TM = BC / WC / 16;
+  constexpr int TN = BP / WP / 16;
+  constexpr int A_IT = BC / 32;
+  constexpr int B_IT = BP / 32;
+  static_assert(WC * WP == 4, "4 waves");
+  static_assert(BC % 32 == 0 && BP % 32 == 0, "tiles of 32");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BC + BP) * 128];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wc = wave / WP, wp = wave % WP;
+  const int hw = p.oh * p.ow;
+  const long long npix = (long long)p.n * hw;
+  const long long p0 = (long long)blockIdx.x * BP;
+  const int c0 = blockIdx.y * BC;
+  const int vec = tid & 7;
+  const int ntap = p.th * p.tw;
+  const int K = ntap * p.c;
+  const int CV = p.c / VEC;
+  const int nk = (K + KSTEP - 1) / KSTEP;
+  const char* __restrict__ xg = (const char*)p.x;
+  const char* __restrict__ wg = (const char*)p.w;
+
+  // staged pixel rows of this thread
+  int bn[B_IT], by[B_IT], bx[B_IT];
+#pragma unroll
+  for (int i = 0; i < B_IT; ++i) {
+    const int row = (tid >> 3) + 32 * i;
+    const long long pix = p0 + row;
+    if (pix < npix) {
+      const int n = (int)(pix / hw);
+      const int r = (int)(pix - (long long)n * hw);
+      const int oy = r / p.ow;
+      const int ox = r - oy * p.ow;
+      bn[i] = n;
+      by[i] = oy * p.sy;
+      bx[i] = ox * p.sx;
+    } else {
+      bn[i] = 0;
+      by[i] = -(1 << 28);
+      bx[i] = 0;
+    }
+  }
+  int tap = vec / CV, cv = vec - (vec / CV) * CV;
+
+  i32x4 ra[A_IT], rb[B_IT];
+  auto load_stage = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      const int co = c0 + row;
+      if (co < p.cout)
+        ra[i] = *(const i32x4*)(wg + ((long long)co * p.kpad + (long long)kt * KSTEP + vec * VEC) * ES);
+      else
+        ra[i] = i32x4{0, 0, 0, 0};
+    }
+    const bool tv = tap < ntap;
+    const int ti = tv ? tap / p.tw : 0;
+    const int tj = tap - ti * p.tw;
+    const int dy = p.dy0 + ti * p.ddy, dx = p.dx0 + tj * p.ddx;
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      const int iy = by[i] + dy, ix = bx[i] + dx;
+      if (tv && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw) {
+        const long long off = ((((long long)bn[i] * p.ih + iy) * p.iw + ix) * p.x_ld + (long long)cv * VEC) * ES;
+        rb[i] = *(const i32x4*)(xg + off);
+      } else {
+        rb[i] = i32x4{0, 0, 0, 0};
+      }
+    }
+    cv += 8;
+    while (cv >= CV) {
+      cv -= CV;
+      ++tap;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    char* As = smem + buf * (BC + BP) * 128;
+    char* Bs = As + BC * 128;
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *(i32x4*)(As + swz128(row, vec)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *(i32x4*)(Bs + swz128(row, vec)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+
+  const int r16 = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_stage(kt + 1);
+    const char* As = smem + cur * (BC + BP) * 128;
+    const char* Bs = As + BC * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = 4 * s + (lane >> 4);
+      i32x4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wc * (BC / WC) + 16 * i + r16;
+        af[i] = *(const i32x4*)(As + swz128(row, ch));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wp * (BP / WP) + 16 * j + r16;
+        bf[j] = *(const i32x4*)(Bs + swz128(row, ch));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma_chunk<T>(acc[i][j], af[i], bf[j]);
+    }
+    if (kt + 1 < nk) store_stage(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds 4 consecutive output channels of one pixel per tile
+  OutT* __restrict__ yg = (OutT*)p.y;
+  const OutT* __restrict__ rg = (const OutT*)p.res;
+  const T* __restrict__ zg = (const T*)p.z;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const long long pix = p0 + wp * (BP / WP) + 16 * j + r16;
+    if (pix >= npix) continue;
+    const int n = (int)(pix / hw);
+    const int r = (int)(pix - (long long)n * hw);
+    const int oy = r / p.ow;
+    const int ox = r - oy * p.ow;
+    const long long yrow = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int co = c0 + wc * (BC / WC) + 16 * i + 4 * (lane >> 4);
+      if (co >= p.cout) continue;
+      f32x4 v = acc[i][j];
+      if (p.bias) {
+        v[0] += p.bias[co];
+        v[1] += p.bias[co + 1];
+        v[2] += p.bias[co + 2];
+        v[3] += p.bias[co + 3];
+      }
+      if (rg) v += V4<OutT>::load(rg + yrow * p.res_ld + co);
+      if (p.beta) v += V4<OutT>::load(yg + yrow * p.y_ld + co);
+      if (p.act) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act, p.alpha);
+      }
+      if (p.dact) {
+        const f32x4 z = V4<T>::load(zg + yrow * p.z_ld + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= act_dz(z[e], p.dact, p.alpha);
+      }
+      V4<OutT>::store(yg + yrow * p.y_ld + co, v);
+    }
+  }
+}
+
+template <typename T, int BC, int BP, int WC, int WP>
+static void launch_conv(const dvie_conv_desc& p, hipStream_t s) {
+  const long long npix = (long long)p.n * p.oh * p.ow;
+  dim3 grid((unsigned)((npix + BP - 1) / BP), (unsigned)((p.cout + BC - 1) / BC));
+  if (p.out_f32)
+    hipLaunchKernelGGL((conv_igemm_kernel<T, BC, BP, WC, WP, true>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<T, BC, BP, WC, WP, false>), grid, dim3(256), 0, s, p);
+}
+
+template <typename T>
+static void dispatch_conv(const dvie_conv_desc& p, hipStream_t s) {
+  const long long npix = (long long)p.n * p.oh * p.ow;
+  const bool small = npix < 64LL * 512;  // not enough 128-pixel tiles to fill 256 CUs
+  if (p.cout <= 32) {
+    if (small) launch_conv<T, 32, 64, 2, 2>(p, s);
+    else launch_conv<T, 32, 128, 2, 2>(p, s);
+  } else if (p.cout <= 64) {
+    if (small) launch_conv<T, 64, 64, 2, 2>(p, s);
+    else launch_conv<T, 64, 128, 2, 2>(p, s);
+  } else {
+    if (small) launch_conv<T, 128, 64, 2, 2>(p, s);
+    else launch_conv<T, 128, 128, 2, 2>(p, s);
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// weight gradient
+// ----------------------------------------------------------------------------------
+// bf16 image: [64 pixels][64 channels] = 128-byte rows, 32-byte blocks XOR-swizzled so
+// that the 8 rows read by a half-wave's ds_read_b64_tr_b16 cover all 64 banks.
+__device__ __forceinline__ int wsw_f(int row) { return ((row >> 1) & 1) | ((row >> 2) & 2); }
+__device__ __forceinline__ int wswz(int row, int blk) { return row * 128 + ((blk ^ wsw_f(row)) << 5); }
+
+template <typename T>
+struct WgCfg;
+template <>
+struct WgCfg<bf16_t> {
+  static constexpr int BKP = 64;      // pixels per stage
+  static constexpr int ROWB = 128;    // bytes per LDS row (64 channels)
+  static constexpr int CHR = 8;       // 16-byte chunks per row
+};
+template <>
+struct WgCfg<float> {
+  static constexpr int BKP = 32;
+  static constexpr int ROWB = 320;    // 64 floats + 16 floats pad
+  static constexpr int CHR = 16;
+};
+
+struct PixCursor {
+  int n, oy, ox;  // current pixel of this staged row
+  bool valid;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_kernel(const dvie_wgrad_desc p, long long chunk) {
+  constexpr int BM = 64, BN = 64;
+  constexpr int ES = sizeof(T);
+  constexpr int VEC = 16 / ES;
+  constexpr int BKP = WgCfg<T>::BKP;
+  constexpr int ROWB = WgCfg<T>::ROWB;
+  constexpr int CHR = WgCfg<T>::CHR;
+  constexpr int IT = BKP * CHR / 256;  // 16B chunks per thread per operand = 2
+  constexpr int RSTEP = 256 / CHR;     // rows advanced between a thread's chunks
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * BKP * ROWB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int split = blockIdx.x;
+  const int ntn = (p.c + BN - 1) / BN;
+  const int m0 = (blockIdx.y / ntn) * BM;
+  const int n0 = (blockIdx.y % ntn) * BN;
+  const int tap = blockIdx.z;
+  const int ti = tap / p.tw, tj = tap - (tap / p.tw) * p.tw;
+  const int dy = p.dy0 + ti * p.ddy, dx = p.dx0 + tj * p.ddx;
+  const int hw = p.oh * p.ow;
+  const long long npix = (long long)p.n * hw;
+  const long long pbeg = (long long)split * chunk;
+  const long long pend = pbeg + chunk < npix ? pbeg + chunk : npix;
+  const int nk = pbeg < pend ? (int)((pend - pbeg + BKP - 1) / BKP) : 0;
+  const char* __restrict__ gg = (const char*)p.g;
+  const char* __restrict__ xg = (const char*)p.x;
+
+  const int cc = tid % CHR;        // chunk (channel group) within the row
+  const int row0 = tid / CHR;      // first staged row
+  // running pixel cursors for rows row0 + i*RSTEP
+  long long pix[IT];
+  int cn[IT], coy[IT], cox[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    pix[i] = pbeg + row0 + i * RSTEP;
+    const long long q = pix[i] < npix ? pix[i] : 0;
+    cn[i] = (int)(q / hw);
+    const int r = (int)(q - (long long)cn[i] * hw);
+    coy[i] = r / p.ow;
+    cox[i] = r - coy[i] * p.ow;
+  }
+
+  i32x4 ra[IT], rb[IT];
+  const bool a_ok = (m0 + cc * VEC) < p.cout;
+  const bool b_ok = (n0 + cc * VEC) < p.c;
+  auto load_stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const bool pv = pix[i] < pend;
+      if (pv && a_ok) {
+        const long long off = (pix[i] * p.g_ld + m0 + cc * VEC) * ES;
+        ra[i] = *(const i32x4*)(gg + off);
+      } else {
+        ra[i] = i32x4{0, 0, 0, 0};
+      }
+      const int iy = coy[i] * p.sy + dy, ix = cox[i] * p.sx + dx;
+      if (pv && b_ok && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw) {
+        const long long off = ((((long long)cn[i] * p.ih + iy) * p.iw + ix) * p.x_ld + n0 + cc * VEC) * ES;
+        rb[i] = *(const i32x4*)(xg + off);
+      } else {
+        rb[i] = i32x4{0, 0, 0, 0};
+      }
+      // advance this row's pixel by BKP
+      pix[i] += BKP;
+      cox[i] += BKP;
+      while (cox[i] >= p.ow) {
+        cox[i] -= p.ow;
+        if (++coy[i] >= p.oh) {
+          coy[i] = 0;
+          ++cn[i];
+        }
+      }
+    }
+  };
+  auto store_stage = [&](int buf) {
+    char* As = smem + buf * 2 * BKP * ROWB;
+    char* Bs = As + BKP * ROWB;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int row = row0 + i * RSTEP;
+      int off;
+      if constexpr (sizeof(T) == 2)
+        off = wswz(row, cc >> 1) + ((cc & 1) << 4);
+      else
+        off = row * ROWB + cc * 16;
+      *(i32x4*)(As + off) = ra[i];
+      *(i32x4*)(Bs + off) = rb[i];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load_stage();
+    store_stage(0);
+  }
+  __syncthreads();
+  const int g = lane >> 4, r16 = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_stage();
+    const char* As = smem + cur * 2 * BKP * ROWB;
+    const char* Bs = As + BKP * ROWB;
+    if constexpr (sizeof(T) == 2) {
+      const int q = r16 >> 2, pp = r16 & 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        i32x4 af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int cb = (wm * 32 + 16 * i) >> 4;  // 16-channel block
+          const int rowa = 32 * s + 8 * g + q;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(As + wswz(rowa, cb) + 8 * pp));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(As + wswz(rowa + 4, cb) + 8 * pp));
+          af[i] = i32x4{(int)((uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16)),
+                        (int)((uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16)),
+                        (int)((uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16)),
+                        (int)((uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16))};
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int cb = (wn * 32 + 16 * j) >> 4;
+          const int rowb = 32 * s + 8 * g + q;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Bs + wswz(rowb, cb) + 8 * pp));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Bs + wswz(rowb + 4, cb) + 8 * pp));
+          bf[j] = i32x4{(int)((uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16)),
+                        (int)((uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16)),
+                        (int)((uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16)),
+                        (int)((uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16))};
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                                __builtin_bit_cast(bf16x8, bf[j]), acc[i][j], 0, 0,
+                                                                0);
+      }
+    } else {
+      const float* Af = (const float*)As;
+      const float* Bf = (const float*)Bs;
+      constexpr int RF = ROWB / 4;
+#pragma unroll
+      for (int k = 0; k < BKP; k += 4) {
+        float a0 = Af[(k + g) * RF + wm * 32 + r16];
+        float a1 = Af[(k + g) * RF + wm * 32 + 16 + r16];
+        float b0 = Bf[(k + g) * RF + wn * 32 + r16];
+        float b1 = Bf[(k + g) * RF + wn * 32 + 16 + r16];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) store_stage(cur ^ 1);
+    __syncthreads();
+  }
+
+  // partial slab: ws[split][co][tap*c + ci]
+  const long long kw = (long long)p.th * p.tw * p.c;
+  float* __restrict__ out = p.ws + (long long)split * p.cout * kw;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = n0 + wn * 32 + 16 * j + r16;
+      if (ci >= p.c) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = m0 + wm * 32 + 16 * i + 4 * g + e;
+        if (co < p.cout) out[(long long)co * kw + (long long)tap * p.c + ci] = acc[i][j][e];
+      }
+    }
+}
+
+__global__ void wreduce_kernel(const dvie_wreduce_desc p) {
+  const long long total = (long long)p.cout_p * p.cin_p * p.kh_n * p.kw_n;
+  const long long slab = (long long)p.ws_rows * p.ws_k;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int kw = (int)(e % p.kw_n);
+    long long r = e / p.kw_n;
+    const int kh = (int)(r % p.kh_n);
+    r /= p.kh_n;
+    const int ci = (int)(r % p.cin_p);
+    const int co = (int)(r / p.cin_p);
+    const int cpos = p.cinv ? p.cinv[ci] : ci;
+    const int t = kh * p.kw_n + kw;
+    const float* src = p.ws + (long long)(co + p.co_off) * p.ws_k + (long long)t * p.c + cpos;
+    double s = 0.0;
+    for (int k = 0; k < p.splits; ++k) s += (double)src[k * slab];
+    float v = (float)s;
+    if (p.beta) v += p.dw[e];
+    p.dw[e] = v;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const dvie_colsum_desc p, long long chunk) {
+  __shared__ float red[256 * 4];
+  const int cq = p.c / 4;
+  const int nrl = cq >= 256 ? 1 : 256 / cq;
+  const int tid = threadIdx.x;
+  const long long rbeg = (long long)blockIdx.x * chunk;
+  const long long rend = rbeg + chunk < p.rows ? rbeg + chunk : p.rows;
+  for (int qb = 0; qb < cq; qb += 256 / nrl) {
+    const int q = qb + tid % (256 / nrl);
+    const int rl = tid / (256 / nrl);
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (q < cq && rl < nrl) {
+      for (long long r = rbeg + rl; r < rend; r += nrl) s += V4<T>::load((const T*)p.g + r * p.g_ld + 4 * q);
+    }
+    for (int e = 0; e < 4; ++e) red[tid * 4 + e] = s[e];
+    __syncthreads();
+    if (tid < 256 / nrl && qb + tid < cq) {
+      f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < nrl; ++k)
+        for (int e = 0; e < 4; ++e) t[e] += red[(k * (256 / nrl) + tid) * 4 + e];
+      for (int e = 0; e < 4; ++e) p.ws[(long long)blockIdx.x * p.c + 4 * (qb + tid) + e] = t[e];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void pack_kernel(const dvie_pack_desc* __restrict__ descs) {
+  const dvie_pack_desc p = descs[blockIdx.y];
+  const long long total = (long long)p.rows * p.kpad;
+  const int ntap = p.th * p.tw;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / p.kpad);
+    const int k = (int)(e - (long long)r * p.kpad);
+    const int t = k / p.c;
+    const int j = k - t * p.c;
+    float v = 0.f;
+    if (t < ntap) {
+      int co, ci;
+      if (p.mode == 0) {
+        co = r;
+        ci = p.cmap ? p.cmap[j] : j;
+      } else {
+        co = j;
+        ci = p.cmap ? p.cmap[r] : r;
+      }
+      const int kh = p.kh0 + (t / p.tw) * p.dkh;
+      const int kw = p.kw0 + (t % p.tw) * p.dkw;
+      if (co < p.cout_s && ci >= 0 && ci < p.cin_s && kh >= 0 && kh < p.kh_s && kw >= 0 && kw < p.kw_s)
+        v = p.src[(((long long)co * p.cin_s + ci) * p.kh_s + kh) * p.kw_s + kw];
+    }
+    if (p.dtype == DVIE_BF16)
+      ((bf16_t*)p.dst)[e] = f2bf(v);
+    else
+      ((float*)p.dst)[e] = v;
+  }
+}
+
+}  // namespace dvie
+
+using namespace dvie;
+
+extern "C" {
+
+int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
+  DVIE_CHECK_ARG(d && d->x && d->w && d->y, "conv: null pointer");
+  const int vec = d->dtype == DVIE_BF16 ? 8 : 4;
+  DVIE_CHECK_ARG(d->c > 0 && d->c % vec == 0, "conv: c=%d must be a multiple of %d", d->c, vec);
+  DVIE_CHECK_ARG(d->cout > 0 && d->cout % 4 == 0, "conv: cout=%d must be a multiple of 4", d->cout);
+  DVIE_CHECK_ARG(d->kpad % 64 == 0 && d->kpad >= d->th * d->tw * d->c, "conv: kpad=%d", d->kpad);
+  DVIE_CHECK_ARG(d->x_ld % vec == 0 && d->y_ld % 4 == 0, "conv: ld alignment x_ld=%lld y_ld=%lld",
+                 d->x_ld, d->y_ld);
+  DVIE_CHECK_ARG(d->th >= 1 && d->tw >= 1 && d->th * d->tw <= 64, "conv: taps");
+  DVIE_CHECK_ARG(d->n > 0 && d->oh > 0 && d->ow > 0 && d->ih > 0 && d->iw > 0, "conv: empty shape");
+  DVIE_CHECK_ARG(((uintptr_t)d->x & 15) == 0 && ((uintptr_t)d->w & 15) == 0, "conv: x/w not 16B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == DVIE_BF16)
+    dispatch_conv<bf16_t>(*d, s);
+  else {
+    DVIE_CHECK_ARG(d->out_f32 || d->dtype == DVIE_F32, "conv: dtype");
+    dispatch_conv<float>(*d, s);
+  }
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
+  DVIE_CHECK_ARG(d && d->g && d->x && d->ws, "wgrad: null pointer");
+  const int vec = d->dtype == DVIE_BF16 ? 8 : 4;
+  DVIE_CHECK_ARG(d->c % vec == 0 && d->g_ld % vec == 0 && d->x_ld % vec == 0,
+                 "wgrad: channel alignment c=%d g_ld=%lld x_ld=%lld", d->c, d->g_ld, d->x_ld);
+  DVIE_CHECK_ARG(d->splits >= 1, "wgrad: splits");
+  const long long npix = (long long)d->n * d->oh * d->ow;
+  const int bkp = d->dtype == DVIE_BF16 ? 64 : 32;
+  long long chunk = (npix + d->splits - 1) / d->splits;
+  chunk = (chunk + bkp - 1) / bkp * bkp;
+  dim3 grid((unsigned)d->splits, (unsigned)(((d->cout + 63) / 64) * ((d->c + 63) / 64)), (unsigned)(d->th * d->tw));
+  hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == DVIE_BF16)
+    hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, *d, chunk);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, s, *d, chunk);
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream) {
+  DVIE_CHECK_ARG(d && d->ws && d->dw, "wreduce: null pointer");
+  const long long total = (long long)d->cout_p * d->cin_p * d->kh_n * d->kw_n;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(wreduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *d);
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_colsum(const dvie_colsum_desc* d, void* stream) {
+  DVIE_CHECK_ARG(d && d->g && d->ws && d->c % 4 == 0 && d->c <= 4096, "colsum: args");
+  DVIE_CHECK_ARG(d->g_ld % 4 == 0, "colsum: g_ld");
+  const long long chunk = (d->rows + d->splits - 1) / d->splits;
+  hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == DVIE_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(d->splits), dim3(256), 0, s, *d, chunk);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(d->splits), dim3(256), 0, s, *d, chunk);
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, void* stream) {
+  DVIE_CHECK_ARG(descs_dev && n > 0 && n < 65536, "pack: args");
+  int blocks = (max_elems + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(pack_kernel, dim3(blocks, n), dim3(256), 0, (hipStream_t)stream, descs_dev);
+  DVIE_RETURN_LAUNCH();
+}
+
+const char* dvie_last_error(void) { return dvie::last_error(); }
+
+}  // extern "C"

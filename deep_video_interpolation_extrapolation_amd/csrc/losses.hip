@@ -1,0 +1,438 @@
+// Loss / metric reductions (fp32 math, double cross-block accumulation, deterministic):
+// L1, gradient-difference (GDL), SSIM (11x11 gaussian, separable, LDS-tiled), per-sample
+// MSE (PSNR), softmax cross-entropy against argmax(one-hot), and the VGG feature L1.
+// Each kernel writes per-block partial sums; a one-block kernel folds them into the
+// output scalar(s).  When a gradient buffer is given, the kernels also write
+// d(weight*loss)/d(pred) in NCHW-contiguous fp32 (the autograd wrappers scale it by
+// the incoming gradient).
+//
+// Reference: losses.py:18-48 (_ssim / create_window), 63-87 (SSIM), 103-116 (PSNR),
+// 137-151 (GDLLoss), 157-180 (VGGLoss feature L1), nn.L1Loss (losses.py:224) and
+// nn.CrossEntropyLoss (runners/InterTrainer.py:75,414).
+#include "common.h"
+
+namespace dvie {
+
+constexpr int RB = 256;  // reduction block
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  const int tid = threadIdx.x;
+  // wave reduction
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((tid & 63) == 0) sh[tid >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (tid == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+
+struct Shape {
+  long long sn, sc, sh, sw;
+  __device__ __forceinline__ long long at(int n, int c, int y, int x) const {
+    return (long long)n * sn + (long long)c * sc + (long long)y * sh + (long long)x * sw;
+  }
+};
+
+// elementwise L1 / GDL / MSE over (B, C, H, W) with x fastest
+__global__ __launch_bounds__(RB) void l1gdl_kernel(const dvie_loss_desc p, int per_sample_blocks) {
+  __shared__ double sh[RB / 64];
+  const float* a = (const float*)p.a;
+  const float* b = (const float*)p.b;
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const long long per = (long long)p.ch * p.h * p.w;
+  long long lo = 0, hi = (long long)p.bsz * per, stride = (long long)gridDim.x * blockDim.x;
+  long long start = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (p.kind == DVIE_LOSS_MSE) {  // blocks partitioned per sample
+    const int smp = blockIdx.x / per_sample_blocks;
+    lo = (long long)smp * per;
+    hi = lo + per;
+    start = lo + (long long)(blockIdx.x % per_sample_blocks) * blockDim.x + threadIdx.x;
+    stride = (long long)per_sample_blocks * blockDim.x;
+  }
+  const double nx = (double)p.bsz * p.ch * p.h * (p.w - 1), ny = (double)p.bsz * p.ch * (p.h - 1) * p.w;
+  const double nall = (double)p.bsz * per;
+  double acc = 0.0;
+  for (long long e = start; e < hi; e += stride) {
+    const int x = (int)(e % p.w);
+    const int y = (int)((e / p.w) % p.h);
+    const int c = (int)((e / ((long long)p.w * p.h)) % p.ch);
+    const int n = (int)(e / per);
+    const float av = a[sa.at(n, c, y, x)], bv = b[sb.at(n, c, y, x)];
+    const float d = av - bv;
+    float g = 0.f;
+    if (p.kind == DVIE_LOSS_L1) {
+      acc += fabsf(d);
+      g = sgnf(d) / (float)nall;
+    } else if (p.kind == DVIE_LOSS_MSE) {
+      acc += (double)(d * d);
+    } else {  // GDL
+      float gx = 0.f, gy = 0.f;
+      if (x + 1 < p.w) {
+        const float dx = (a[sa.at(n, c, y, x + 1)] - av) - (b[sb.at(n, c, y, x + 1)] - bv);
+        acc += fabs((double)dx) / (2.0 * nx);
+        gx -= sgnf(dx);
+      }
+      if (x > 0) {
+        const float dxm = (av - a[sa.at(n, c, y, x - 1)]) - (bv - b[sb.at(n, c, y, x - 1)]);
+        gx += sgnf(dxm);
+      }
+      if (y + 1 < p.h) {
+        const float dy = (a[sa.at(n, c, y + 1, x)] - av) - (b[sb.at(n, c, y + 1, x)] - bv);
+        acc += fabs((double)dy) / (2.0 * ny);
+        gy -= sgnf(dy);
+      }
+      if (y > 0) {
+        const float dym = (av - a[sa.at(n, c, y - 1, x)]) - (bv - b[sb.at(n, c, y - 1, x)]);
+        gy += sgnf(dym);
+      }
+      g = (float)(gx / (2.0 * nx) + gy / (2.0 * ny));
+    }
+    if (p.grad && p.kind != DVIE_LOSS_MSE) {
+      const float v = p.weight * g;
+      p.grad[e] = p.beta ? p.grad[e] + v : v;
+    }
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) p.partial[blockIdx.x] = t;
+}
+
+// cross entropy: logits a (B, C, H, W), target one-hot b; one thread per pixel
+__global__ __launch_bounds__(RB) void ce_kernel(const dvie_loss_desc p) {
+  __shared__ double sh[RB / 64];
+  const float* a = (const float*)p.a;
+  const float* b = (const float*)p.b;
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const long long npx = (long long)p.bsz * p.h * p.w;
+  double acc = 0.0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < npx;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(e % p.w);
+    const int y = (int)((e / p.w) % p.h);
+    const int n = (int)(e / ((long long)p.w * p.h));
+    int label = 0;
+    float best = b[sb.at(n, 0, y, x)];
+    float mx = a[sa.at(n, 0, y, x)];
+    for (int c = 1; c < p.ch; ++c) {
+      const float t = b[sb.at(n, c, y, x)];
+      if (t > best) {
+        best = t;
+        label = c;
+      }
+      mx = fmaxf(mx, a[sa.at(n, c, y, x)]);
+    }
+    float s = 0.f;
+    for (int c = 0; c < p.ch; ++c) s += expf(a[sa.at(n, c, y, x)] - mx);
+    const float lse = mx + logf(s);
+    acc += (double)(lse - a[sa.at(n, label, y, x)]);
+    if (p.grad) {
+      const float inv = p.weight / (float)npx;
+      for (int c = 0; c < p.ch; ++c) {
+        const float pr = expf(a[sa.at(n, c, y, x)] - mx) / s;
+        const float v = (pr - (c == label ? 1.f : 0.f)) * inv;
+        const long long gi = (((long long)n * p.ch + c) * p.h + y) * p.w + x;
+        p.grad[gi] = p.beta ? p.grad[gi] + v : v;
+      }
+    }
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) p.partial[blockIdx.x] = t;
+}
+
+// mean |a - b| over two equally shaped strided tensors, channel fastest
+template <typename T>
+__global__ __launch_bounds__(RB) void l1nhwc_kernel(const dvie_loss_desc p) {
+  __shared__ double sh[RB / 64];
+  const T* a = (const T*)p.a;
+  const T* b = (const T*)p.b;
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const long long tot = (long long)p.bsz * p.ch * p.h * p.w;
+  double acc = 0.0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % p.ch);
+    const long long pix = e / p.ch;
+    const int x = (int)(pix % p.w);
+    const int y = (int)((pix / p.w) % p.h);
+    const int n = (int)(pix / ((long long)p.w * p.h));
+    float av, bv;
+    if constexpr (sizeof(T) == 2) {
+      av = bf2f(a[sa.at(n, c, y, x)]);
+      bv = bf2f(b[sb.at(n, c, y, x)]);
+    } else {
+      av = a[sa.at(n, c, y, x)];
+      bv = b[sb.at(n, c, y, x)];
+    }
+    acc += fabsf(av - bv);
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) p.partial[blockIdx.x] = t;
+}
+
+// ---------------- SSIM ----------------
+constexpr int ST = 16;        // output tile edge
+constexpr int SR = 5;         // window radius
+constexpr int SE = ST + 2 * SR;
+
+__device__ __forceinline__ void gauss11(float* g) {
+  float s = 0.f;
+  for (int i = 0; i < 11; ++i) {
+    g[i] = expf(-(float)((i - 5) * (i - 5)) / 4.5f);
+    s += g[i];
+  }
+  for (int i = 0; i < 11; ++i) g[i] /= s;
+}
+
+// forward: per-pixel ssim, partial sums, and (if grad) the three adjoint maps
+// alpha = dL/dmu1, beta = dL/dE11, gamma = dL/dE12 into ws
+__global__ __launch_bounds__(256) void ssim_fwd_kernel(const dvie_loss_desc p) {
+  __shared__ float g[11];
+  __shared__ float t1[SE][SE], t2[SE][SE];
+  __shared__ float hs[5][SE][ST];
+  __shared__ double sh[4];
+  const float* a = (const float*)p.a;
+  const float* b = (const float*)p.b;
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const int tid = threadIdx.x;
+  const int tx = tid % ST, ty = tid / ST;
+  const int plane = blockIdx.z;
+  const int n = plane / p.ch, c = plane % p.ch;
+  const int x0 = blockIdx.x * ST, y0 = blockIdx.y * ST;
+  if (tid == 0) gauss11(g);
+  for (int i = tid; i < SE * SE; i += 256) {
+    const int yy = i / SE, xx = i % SE;
+    const int gy = y0 + yy - SR, gx = x0 + xx - SR;
+    float va = 0.f, vb = 0.f;
+    if (gy >= 0 && gy < p.h && gx >= 0 && gx < p.w) {
+      va = a[sa.at(n, c, gy, gx)];
+      vb = b[sb.at(n, c, gy, gx)];
+    }
+    t1[yy][xx] = va;
+    t2[yy][xx] = vb;
+  }
+  __syncthreads();
+  for (int i = tid; i < SE * ST; i += 256) {
+    const int yy = i / ST, xx = i % ST;
+    float s1 = 0.f, s2 = 0.f, s11 = 0.f, s22 = 0.f, s12 = 0.f;
+    for (int k = 0; k < 11; ++k) {
+      const float u = t1[yy][xx + k], v = t2[yy][xx + k], w = g[k];
+      s1 += w * u;
+      s2 += w * v;
+      s11 += w * u * u;
+      s22 += w * v * v;
+      s12 += w * u * v;
+    }
+    hs[0][yy][xx] = s1;
+    hs[1][yy][xx] = s2;
+    hs[2][yy][xx] = s11;
+    hs[3][yy][xx] = s22;
+    hs[4][yy][xx] = s12;
+  }
+  __syncthreads();
+  float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+  for (int k = 0; k < 11; ++k) {
+    const float w = g[k];
+    m1 += w * hs[0][ty + k][tx];
+    m2 += w * hs[1][ty + k][tx];
+    e11 += w * hs[2][ty + k][tx];
+    e22 += w * hs[3][ty + k][tx];
+    e12 += w * hs[4][ty + k][tx];
+  }
+  const int oy = y0 + ty, ox = x0 + tx;
+  double acc = 0.0;
+  if (oy < p.h && ox < p.w) {
+    const float C1 = 0.01f * 0.01f, C2 = 0.03f * 0.03f;
+    const float s11 = e11 - m1 * m1, s22 = e22 - m2 * m2, s12 = e12 - m1 * m2;
+    const float A = 2.f * m1 * m2 + C1, B = 2.f * s12 + C2;
+    const float Cc = m1 * m1 + m2 * m2 + C1, D = s11 + s22 + C2;
+    const float S = (A * B) / (Cc * D);
+    acc = S;
+    if (p.grad) {
+      const float inv = -1.f / ((float)p.bsz * p.ch * p.h * p.w);
+      const float dm1 = S * (2.f * m2 / A - 2.f * m2 / B - 2.f * m1 / Cc + 2.f * m1 / D);
+      const float de11 = -S / D;
+      const float de12 = 2.f * S / B;
+      const long long plane_sz = (long long)p.h * p.w;
+      const long long np = (long long)p.bsz * p.ch * plane_sz;
+      const long long idx = (long long)plane * plane_sz + (long long)oy * p.w + ox;
+      p.ws[idx] = inv * dm1;
+      p.ws[np + idx] = inv * de11;
+      p.ws[2 * np + idx] = inv * de12;
+    }
+  }
+  const double t = block_sum(acc, sh);
+  if (tid == 0) p.partial[((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = t;
+}
+
+// backward: dx1 = G*alpha + 2 x1 (G*beta) + x2 (G*gamma)
+__global__ __launch_bounds__(256) void ssim_bwd_kernel(const dvie_loss_desc p) {
+  __shared__ float g[11];
+  __shared__ float t[3][SE][SE];
+  __shared__ float hs[3][SE][ST];
+  const float* a = (const float*)p.a;
+  const float* b = (const float*)p.b;
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const int tid = threadIdx.x;
+  const int tx = tid % ST, ty = tid / ST;
+  const int plane = blockIdx.z;
+  const int n = plane / p.ch, c = plane % p.ch;
+  const int x0 = blockIdx.x * ST, y0 = blockIdx.y * ST;
+  const long long plane_sz = (long long)p.h * p.w;
+  const long long np = (long long)p.bsz * p.ch * plane_sz;
+  if (tid == 0) gauss11(g);
+  for (int i = tid; i < SE * SE; i += 256) {
+    const int yy = i / SE, xx = i % SE;
+    const int gy = y0 + yy - SR, gx = x0 + xx - SR;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (gy >= 0 && gy < p.h && gx >= 0 && gx < p.w) {
+      const long long idx = (long long)plane * plane_sz + (long long)gy * p.w + gx;
+      v0 = p.ws[idx];
+      v1 = p.ws[np + idx];
+      v2 = p.ws[2 * np + idx];
+    }
+    t[0][yy][xx] = v0;
+    t[1][yy][xx] = v1;
+    t[2][yy][xx] = v2;
+  }
+  __syncthreads();
+  for (int i = tid; i < SE * ST; i += 256) {
+    const int yy = i / ST, xx = i % ST;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int k = 0; k < 11; ++k) {
+      s0 += g[k] * t[0][yy][xx + k];
+      s1 += g[k] * t[1][yy][xx + k];
+      s2 += g[k] * t[2][yy][xx + k];
+    }
+    hs[0][yy][xx] = s0;
+    hs[1][yy][xx] = s1;
+    hs[2][yy][xx] = s2;
+  }
+  __syncthreads();
+  float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+  for (int k = 0; k < 11; ++k) {
+    u0 += g[k] * hs[0][ty + k][tx];
+    u1 += g[k] * hs[1][ty + k][tx];
+    u2 += g[k] * hs[2][ty + k][tx];
+  }
+  const int oy = y0 + ty, ox = x0 + tx;
+  if (oy < p.h && ox < p.w) {
+    const float x1 = a[sa.at(n, c, oy, ox)], x2 = b[sb.at(n, c, oy, ox)];
+    const float v = p.weight * (u0 + 2.f * x1 * u1 + x2 * u2);
+    const long long gi = (long long)plane * plane_sz + (long long)oy * p.w + ox;
+    p.grad[gi] = p.beta ? p.grad[gi] + v : v;
+  }
+}
+
+__global__ __launch_bounds__(RB) void finalize_kernel(const double* part, int nb, int nout, float* out, double mul,
+                                                      double add) {
+  __shared__ double sh[RB / 64];
+  for (int j = 0; j < nout; ++j) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[(long long)j * nb + i];
+    const double t = block_sum(s, sh);
+    if (threadIdx.x == 0) out[j] = (float)(t * mul + add);
+  }
+}
+
+struct LossPlan {
+  int blocks;       // partial count
+  int per_sample;   // MSE: blocks per sample
+  dim3 grid;
+};
+
+static LossPlan plan_loss(const dvie_loss_desc& d) {
+  LossPlan lp{};
+  const long long px = (long long)d.bsz * d.h * d.w;
+  const long long tot = px * d.ch;
+  switch (d.kind) {
+    case DVIE_LOSS_SSIM:
+      lp.grid = dim3((d.w + ST - 1) / ST, (d.h + ST - 1) / ST, d.bsz * d.ch);
+      lp.blocks = lp.grid.x * lp.grid.y * lp.grid.z;
+      break;
+    case DVIE_LOSS_MSE: {
+      long long per = (long long)d.ch * d.h * d.w;
+      int ps = (int)((per + RB * 8 - 1) / (RB * 8));
+      if (ps > 256) ps = 256;
+      if (ps < 1) ps = 1;
+      lp.per_sample = ps;
+      lp.blocks = ps * d.bsz;
+      lp.grid = dim3(lp.blocks);
+      break;
+    }
+    case DVIE_LOSS_CE: {
+      long long b = (px + RB * 4 - 1) / (RB * 4);
+      lp.blocks = (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
+      lp.grid = dim3(lp.blocks);
+      break;
+    }
+    default: {
+      long long b = (tot + RB * 8 - 1) / (RB * 8);
+      lp.blocks = (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
+      lp.grid = dim3(lp.blocks);
+      break;
+    }
+  }
+  return lp;
+}
+
+}  // namespace dvie
+
+using namespace dvie;
+
+extern "C" {
+
+size_t dvie_loss_partial_count(const dvie_loss_desc* d) { return d ? (size_t)plan_loss(*d).blocks : 0; }
+
+size_t dvie_loss_ws_floats(const dvie_loss_desc* d) {
+  if (!d || d->kind != DVIE_LOSS_SSIM) return 0;
+  return (size_t)3 * d->bsz * d->ch * d->h * d->w;
+}
+
+int dvie_loss(const dvie_loss_desc* d, void* stream) {
+  DVIE_CHECK_ARG(d && d->a && d->b && d->out && d->partial, "loss: null pointer");
+  DVIE_CHECK_ARG(d->bsz > 0 && d->ch > 0 && d->h > 0 && d->w > 0, "loss: empty shape");
+  if (d->kind == DVIE_LOSS_GDL) DVIE_CHECK_ARG(d->h > 1 && d->w > 1, "loss: GDL needs h,w > 1");
+  if (d->kind == DVIE_LOSS_SSIM && d->grad) DVIE_CHECK_ARG(d->ws != nullptr, "loss: SSIM grad needs ws");
+  hipStream_t s = (hipStream_t)stream;
+  const LossPlan lp = plan_loss(*d);
+  const double px = (double)d->bsz * d->h * d->w;
+  const double tot = px * d->ch;
+  switch (d->kind) {
+    case DVIE_LOSS_L1:
+    case DVIE_LOSS_GDL:
+      hipLaunchKernelGGL(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, 0);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
+                         d->kind == DVIE_LOSS_L1 ? 1.0 / tot : 1.0, 0.0);
+      break;
+    case DVIE_LOSS_MSE:
+      hipLaunchKernelGGL(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, lp.per_sample);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.per_sample, d->bsz, d->out,
+                         1.0 / ((double)d->ch * d->h * d->w), 0.0);
+      break;
+    case DVIE_LOSS_CE:
+      hipLaunchKernelGGL(ce_kernel, lp.grid, dim3(RB), 0, s, *d);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0);
+      break;
+    case DVIE_LOSS_SSIM:
+      hipLaunchKernelGGL(ssim_fwd_kernel, lp.grid, dim3(256), 0, s, *d);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, -1.0 / tot,
+                         1.0);
+      if (d->grad) hipLaunchKernelGGL(ssim_bwd_kernel, lp.grid, dim3(256), 0, s, *d);
+      break;
+    case DVIE_LOSS_L1NHWC:
+      if (d->dtype == DVIE_BF16)
+        hipLaunchKernelGGL(l1nhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d);
+      else
+        hipLaunchKernelGGL(l1nhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / tot, 0.0);
+      break;
+    default:
+      DVIE_CHECK_ARG(false, "loss: unknown kind %d", d->kind);
+  }
+  DVIE_RETURN_LAUNCH();
+}
+
+}  // extern "C"

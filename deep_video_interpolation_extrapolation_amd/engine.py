@@ -1,0 +1,792 @@
+"""Plan compiler for the MI355X frame-synthesis path.
+
+A network (HRNet coarse generator, VGG19 perceptual features, ...) is described once with
+a small builder API (`Graph.conv / fuse / pool / input_nchw / l1feat`).  `Graph.compile`
+turns it into two flat descriptor lists for the C ABI (include/dvie.h):
+
+* forward:  weight packing (one launch for all layers) + one descriptor per op;
+* backward: derived here by reverse traversal.  Gradient contributions to a buffer are
+  collected and emitted only when the last one is known, so that
+  - the first contribution overwrites and the rest accumulate (epilogue `beta`),
+  - identity contributions (residual adds, same-resolution fuse terms) ride along as the
+    `res` operand of a kernel contribution instead of costing a pass of their own,
+  - the producer's activation derivative (LeakyReLU/ELU/ReLU, computed from its output)
+    is applied by the epilogue of the last contribution, so every buffer's gradient is
+    already the pre-activation gradient the producer's wgrad/dgrad need.
+
+Each list runs with a single host call (`dvie_run_ops`) on the current HIP stream.
+All activations are NHWC buffers allocated once per (batch, height, width) plan; the
+kernels never allocate.  Reference semantics: nets/HRNet.py, nets/vgg.py, losses.py.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib as L
+
+PADC = 8  # channel padding granule (16-byte bf16 vectors)
+
+
+def rup(x, m):
+    return (x + m - 1) // m * m
+
+
+def elem_size(dt):
+    return 2 if dt == torch.bfloat16 else 4
+
+
+def dv_dtype(dt):
+    return L.BF16 if dt == torch.bfloat16 else L.F32
+
+
+class Buffer:
+    """NHWC activation buffer [N, H, W, C] (C is also the pixel stride)."""
+
+    def __init__(self, name, H, W, C, dtype=None, external=False):
+        self.name, self.H, self.W, self.C = name, H, W, C
+        self.dtype = dtype  # None -> graph compute dtype
+        self.external = external
+        self.t = None  # forward storage
+        self.g = None  # gradient storage [Nb, H, W, C] (compute dtype)
+        self.needs_grad = False
+        self.producers = []
+        self.consumers = []  # (op, region)
+        self.expected = 0
+        self.pending = []
+        self.read_region = None
+
+    def __repr__(self):
+        return f"Buffer({self.name},{self.H}x{self.W}x{self.C})"
+
+
+class Region:
+    """Channel slice [c0, c0 + c) of a buffer."""
+
+    def __init__(self, buf, c0=0, c=None):
+        self.buf, self.c0 = buf, c0
+        self.c = buf.C - c0 if c is None else c
+        assert 0 <= c0 and c0 + self.c <= buf.C, (buf, c0, c)
+
+    def key(self):
+        return (self.c0, self.c)
+
+    @property
+    def H(self):
+        return self.buf.H
+
+    @property
+    def W(self):
+        return self.buf.W
+
+
+def R(buf, c0=0, c=None):
+    return Region(buf, c0, c)
+
+
+class ConvLayer:
+    """Packing/gradient metadata for one nn.Conv2d-shaped parameter set (OIHW fp32)."""
+
+    def __init__(self, module, trainable=True, name=""):
+        self.m = module
+        self.name = name
+        w = module.weight
+        self.cout, self.cin, self.kh, self.kw = w.shape
+        self.stride = module.stride[0]
+        self.pad = module.padding[0]
+        assert module.stride[0] == module.stride[1] and module.padding[0] == module.padding[1]
+        assert module.dilation == (1, 1) and module.groups == 1
+        self.has_bias = module.bias is not None
+        self.trainable = trainable
+        self.cmap = None  # packed input position -> source input channel (or -1)
+        self.cin_p = None  # packed input channels
+        self.cout_p = rup(self.cout, PADC)
+        self.wf = None  # packed forward weights
+        self.wd = []  # per dgrad phase: (tensor, taps(dict))
+        self.bias_p = None
+        self.uses = 0
+
+    def bind_input(self, cin_p, cmap):
+        if cmap is None:
+            cmap = list(range(self.cin)) + [-1] * (cin_p - self.cin)
+        assert len(cmap) == cin_p and cin_p >= self.cin
+        if self.cin_p is None:
+            self.cin_p, self.cmap = cin_p, list(cmap)
+        else:
+            assert self.cin_p == cin_p and self.cmap == list(cmap), f"{self.name}: inconsistent input packing"
+
+    def fwd_taps(self):
+        return dict(th=self.kh, tw=self.kw, dy0=-self.pad, dx0=-self.pad, ddy=1, ddx=1, kh0=0, kw0=0, dkh=1, dkw=1)
+
+    def dgrad_phases(self, H, W):
+        """Stride-s data gradient as s*s stride-1 convs over the output gradient."""
+        s, p = self.stride, self.pad
+        phases = []
+        for ry in range(s):
+            khs = [k for k in range(self.kh) if (ry + p - k) % s == 0]
+            if not khs:
+                continue
+            for rx in range(s):
+                kws = [k for k in range(self.kw) if (rx + p - k) % s == 0]
+                if not kws:
+                    continue
+                oh = (H - ry + s - 1) // s
+                ow = (W - rx + s - 1) // s
+                if oh <= 0 or ow <= 0:
+                    continue
+                phases.append(dict(ry=ry, rx=rx, oh=oh, ow=ow, th=len(khs), tw=len(kws), kh0=khs[0], kw0=kws[0],
+                                   dkh=s, dkw=s, dy0=(ry + p - khs[0]) // s, dx0=(rx + p - kws[0]) // s,
+                                   ddy=-1, ddx=-1))
+        return phases
+
+
+class _Op:
+    pass
+
+
+class ConvOp(_Op):
+    def __init__(self, x, layer, out, act, res):
+        self.x, self.layer, self.out, self.act, self.res = x, layer, out, act, res
+
+    def inputs(self):
+        return [self.x] + ([self.res] if self.res is not None else [])
+
+
+class FuseOp(_Op):
+    def __init__(self, srcs, out, act):
+        self.srcs, self.out, self.act = srcs, out, act
+
+    def inputs(self):
+        return list(self.srcs)
+
+
+class PoolOp(_Op):
+    def __init__(self, x, out):
+        self.x, self.out, self.act = x, out, L.ACT_NONE
+
+    def inputs(self):
+        return [self.x]
+
+
+class InputOp(_Op):
+    """NCHW fp32 external tensor -> NHWC region.  `part` None: the whole batch;
+    0 / 1: first / second half of the plan batch (VGG runs [pred | target])."""
+
+    def __init__(self, out, key, part, ext_c0, ext_c, normalize, requires_grad):
+        self.out, self.key, self.part, self.ext_c0, self.ext_c = out, key, part, ext_c0, ext_c
+        self.normalize, self.requires_grad, self.act = normalize, requires_grad, L.ACT_NONE
+
+    def inputs(self):
+        return []
+
+
+class L1FeatOp(_Op):
+    """mean |f(pred) - f(gt)| of a feature buffer holding [pred batch | gt batch]."""
+
+    def __init__(self, a, idx, weight):
+        self.a, self.idx, self.weight, self.out, self.act = a, idx, weight, None, L.ACT_NONE
+
+    def inputs(self):
+        return [self.a]
+
+
+_IMAGENET_MEAN = [0.485, 0.456, 0.406]
+_IMAGENET_STD = [0.229, 0.224, 0.225]
+
+
+class Graph:
+    def __init__(self, dtype=torch.float32):
+        self.dtype = dtype
+        self.ops = []
+        self.buffers = []
+        self.layers = []
+        self.outputs = {}
+        self.n_l1 = 0
+
+    # ---------------- builder ----------------
+    def buffer(self, name, H, W, C, dtype=None, external=False):
+        b = Buffer(name, H, W, C, dtype, external)
+        self.buffers.append(b)
+        return b
+
+    def layer(self, module, trainable=True, name=""):
+        for lay in self.layers:
+            if lay.m is module:
+                return lay
+        lay = ConvLayer(module, trainable, name)
+        self.layers.append(lay)
+        return lay
+
+    def input_nchw(self, out, key, part=None, ext_c0=0, ext_c=None, normalize=False, requires_grad=False):
+        assert not (requires_grad and part == 1)
+        op = InputOp(out, key, part, ext_c0, out.c if ext_c is None else ext_c, normalize, requires_grad)
+        self._add(op)
+        return out
+
+    def conv(self, x, module, out, act=L.ACT_NONE, res=None, cmap=None, trainable=True, name=""):
+        lay = self.layer(module, trainable, name)
+        lay.bind_input(x.c, cmap)
+        assert out.c == lay.cout_p, (name, out.c, lay.cout_p)
+        oh = (x.H + 2 * lay.pad - lay.kh) // lay.stride + 1
+        ow = (x.W + 2 * lay.pad - lay.kw) // lay.stride + 1
+        assert (out.H, out.W) == (oh, ow), (name, out.H, out.W, oh, ow)
+        if res is not None:
+            assert (res.H, res.W, res.c) == (out.H, out.W, out.c)
+        self._add(ConvOp(x, lay, out, act, res))
+        return out
+
+    def fuse(self, srcs, out, act=L.ACT_NONE):
+        assert 1 <= len(srcs) <= 3
+        for s in srcs:
+            assert s.c == out.c
+        self._add(FuseOp(srcs, out, act))
+        return out
+
+    def pool(self, x, out):
+        assert (out.H * 2, out.W * 2, out.c) == (x.H, x.W, x.c)
+        self._add(PoolOp(x, out))
+        return out
+
+    def l1feat(self, a, weight=1.0):
+        op = L1FeatOp(a, self.n_l1, weight)
+        self.n_l1 += 1
+        self._add(op)
+        return op.idx
+
+    def output(self, key, region, channels):
+        self.outputs[key] = (region, channels)
+
+    def _add(self, op):
+        self.ops.append(op)
+        if op.out is not None:
+            op.out.buf.producers.append(op)
+        for r in op.inputs():
+            r.buf.consumers.append((op, r))
+
+    # ---------------- compile ----------------
+    def compile(self, n_fwd, device, n_bwd=None, backward=True):
+        return Plan(self, n_fwd, n_fwd if n_bwd is None else n_bwd, device, backward)
+
+
+class Plan:
+    """Allocated buffers + forward/backward descriptor lists of one graph and shape."""
+
+    def __init__(self, g, nf, nb, device, backward):
+        self.g, self.nf, self.nb, self.device = g, nf, nb, device
+        self.dtype = g.dtype
+        self.dt = dv_dtype(g.dtype)
+        self.es = elem_size(g.dtype)
+        self.vec = 16 // self.es
+        self.backward_enabled = backward
+        self.keep = []  # tensors referenced by raw pointers
+        self.busy = False
+        self.generation = 0
+        self._alloc()
+        self.fwd = []
+        self.bwd = []
+        self.ext_in = {}  # key -> list of (op index, InputOp) for patching
+        self.ext_out = {}
+        self.ext_grad = {}  # key -> list of bwd op indices (TONCHW)
+        self._grad_slots = []  # (bwd index, layer, 'weight'|'bias', first use)
+        self.ext_ograd = {}  # output key -> bwd op index of its gradient pack
+        self.ws_floats = 1
+        self._build_pack()
+        self._build_forward()
+        if backward:
+            self._build_backward()
+        self._finalize()
+
+    # ---------------- allocation ----------------
+    def _alloc(self):
+        g = self.g
+        for b in g.buffers:
+            dt = b.dtype or self.dtype
+            b.dt = dt
+            if b.external:
+                b.t = None
+            else:
+                b.t = torch.empty((self.nf, b.H, b.W, b.C), dtype=dt, device=self.device)
+        # gradient requirements
+        if self.backward_enabled:
+            for op in g.ops:
+                if op.out is None:
+                    continue
+                need = False
+                if isinstance(op, InputOp):
+                    need = op.requires_grad
+                elif isinstance(op, ConvOp):
+                    need = op.layer.trainable or any(r.buf.needs_grad for r in op.inputs())
+                else:
+                    need = any(r.buf.needs_grad for r in op.inputs())
+                op.out.buf.needs_grad = op.out.buf.needs_grad or need
+            for b in g.buffers:
+                if b.needs_grad:
+                    b.g = torch.zeros((self.nb, b.H, b.W, b.C), dtype=self.dtype, device=self.device)
+            for b in g.buffers:
+                b.expected = 0
+                b.pending = []
+                b.read_region = None
+                b.done = False
+            for op in g.ops:
+                for r in op.inputs():
+                    if r.buf.needs_grad:
+                        r.buf.expected += 1
+                        if r.buf.read_region is None:
+                            r.buf.read_region = r.key()
+                        assert r.buf.read_region == r.key(), f"{r.buf}: consumers read different regions"
+        self.l1_out = torch.zeros(max(1, g.n_l1), dtype=torch.float32, device=self.device)
+        self.keep.append(self.l1_out)
+
+    def ptr(self, region, n0=0, grad=False):
+        b = region.buf
+        t = b.g if grad else b.t
+        es = elem_size(t.dtype)
+        return t.data_ptr() + (n0 * b.H * b.W * b.C + region.c0) * es
+
+    # ---------------- weight packing ----------------
+    def _build_pack(self):
+        descs = []
+        for lay in self.g.layers:
+            if lay.cin_p is None:
+                continue
+            K = lay.kh * lay.kw * lay.cin_p
+            kpad = rup(K, 64)
+            lay.kpad = kpad
+            lay.wf = torch.zeros((lay.cout_p, kpad), dtype=self.dtype, device=self.device)
+            cmap_t = torch.tensor(lay.cmap, dtype=torch.int32, device=self.device)
+            lay.cmap_t = cmap_t
+            inv = [0] * lay.cin
+            for pos, ci in enumerate(lay.cmap):
+                if ci >= 0:
+                    inv[ci] = pos
+            lay.cinv_t = torch.tensor(inv, dtype=torch.int32, device=self.device)
+            self.keep += [lay.wf, cmap_t, lay.cinv_t]
+            ft = lay.fwd_taps()
+            descs.append(self._pack_desc(lay, lay.wf, lay.cout_p, kpad, lay.cin_p, 0, ft, cmap_t))
+            if lay.has_bias:
+                lay.bias_p = torch.zeros(lay.cout_p, dtype=torch.float32, device=self.device)
+                self.keep.append(lay.bias_p)
+                d = L.PackDesc()
+                d.src, d.dst, d.cmap = lay.m.bias.data_ptr(), lay.bias_p.data_ptr(), None
+                d.rows, d.kpad, d.c, d.mode = lay.cout_p, 1, 1, 0
+                d.th, d.tw, d.kh0, d.kw0, d.dkh, d.dkw = 1, 1, 0, 0, 1, 1
+                d.cout_s, d.cin_s, d.kh_s, d.kw_s, d.dtype = lay.cout, 1, 1, 1, L.F32
+                descs.append(d)
+            lay.wd = []
+        self._pack_descs = descs  # dgrad packs appended during backward build
+
+    def _pack_desc(self, lay, dst, rows, kpad, c, mode, taps, cmap_t):
+        d = L.PackDesc()
+        d.src, d.dst, d.cmap = lay.m.weight.data_ptr(), dst.data_ptr(), cmap_t.data_ptr()
+        d.rows, d.kpad, d.c, d.mode = rows, kpad, c, mode
+        d.th, d.tw, d.kh0, d.kw0, d.dkh, d.dkw = taps["th"], taps["tw"], taps["kh0"], taps["kw0"], taps["dkh"], taps["dkw"]
+        d.cout_s, d.cin_s, d.kh_s, d.kw_s, d.dtype = lay.cout, lay.cin, lay.kh, lay.kw, self.dt
+        return d
+
+    def _dgrad_weights(self, lay, H, W):
+        """packed [cin_p][kpad] weights for each stride phase (cached per layer/shape)."""
+        key = (H, W)
+        for k, v in lay.wd:
+            if k == key:
+                return v
+        out = []
+        for ph in lay.dgrad_phases(H, W):
+            kpad = rup(ph["th"] * ph["tw"] * lay.cout_p, 64)
+            t = torch.zeros((lay.cin_p, kpad), dtype=self.dtype, device=self.device)
+            self.keep.append(t)
+            self._pack_descs.append(self._pack_desc(lay, t, lay.cin_p, kpad, lay.cout_p, 1, ph, lay.cmap_t))
+            out.append((ph, t, kpad))
+        lay.wd.append((key, out))
+        return out
+
+    # ---------------- descriptor factories ----------------
+    def _op(self, kind):
+        o = L.Op()
+        o.kind = kind
+        return o
+
+    def conv_desc(self, x_ptr, x_ld, n, ih, iw, c, w_ptr, kpad, cout, oh, ow, sy, sx, taps, y_ptr, y_ld, yh, yw,
+                  osy=1, osx=1, ory=0, orx=0, bias=None, res=None, res_ld=0, z=None, z_ld=0, act=0, dact=0, beta=0,
+                  out_f32=False):
+        o = self._op(L.OP_CONV)
+        d = o.u.conv
+        d.x, d.w, d.y, d.bias, d.res, d.z = x_ptr, w_ptr, y_ptr, bias, res, z
+        d.x_ld, d.y_ld, d.res_ld, d.z_ld = x_ld, y_ld, res_ld, z_ld
+        d.n, d.ih, d.iw, d.c, d.kpad, d.cout = n, ih, iw, c, kpad, cout
+        d.oh, d.ow, d.sy, d.sx = oh, ow, sy, sx
+        d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], taps["ddy"], taps["ddx"]
+        d.yh, d.yw, d.osy, d.osx, d.ory, d.orx = yh, yw, osy, osx, ory, orx
+        d.act, d.dact, d.beta, d.dtype, d.out_f32 = act, dact, beta, self.dt, int(out_f32)
+        d.alpha = 0.2
+        return o
+
+    def ew_desc(self, op, n, h, w, c, y_ptr, y_ld, srcs=(), res=None, res_ld=0, z=None, z_ld=0, act=0, dact=0,
+                beta=0, scale=1.0):
+        o = self._op(L.OP_EW)
+        d = o.u.ew
+        d.op, d.n, d.h, d.w, d.c = op, n, h, w, c
+        d.y, d.y_ld = y_ptr, y_ld
+        d.nsrc = len(srcs)
+        for i, (p, ld, sh, sw) in enumerate(srcs):
+            setattr(d, f"src{i}", p)
+            setattr(d, f"src_ld{i}", ld)
+            setattr(d, f"sh{i}", sh)
+            setattr(d, f"sw{i}", sw)
+        d.res, d.res_ld, d.z, d.z_ld = res, res_ld, z, z_ld
+        d.act, d.dact, d.beta, d.dtype = act, dact, beta, self.dt
+        d.alpha, d.scale = 0.2, scale
+        return o
+
+    def _part(self, part):
+        if part is None:
+            return 0, self.nf
+        return (0 if part == 0 else self.nf // 2), self.nf // 2
+
+    # ---------------- forward ----------------
+    def _build_forward(self):
+        g = self.g
+        nf = self.nf
+        for op in g.ops:
+            if isinstance(op, InputOp):
+                n0, cnt = self._part(op.part)
+                o = self.ew_desc(L.EW_NCHW, cnt, op.out.H, op.out.W, op.out.c, self.ptr(op.out, n0), op.out.buf.C)
+                o.u.ew.ext_c = op.ext_c
+                if op.normalize:
+                    m = torch.tensor(_IMAGENET_MEAN + [0.0] * 5, dtype=torch.float32, device=self.device)
+                    s = torch.tensor(_IMAGENET_STD + [1.0] * 5, dtype=torch.float32, device=self.device)
+                    self.keep += [m, s]
+                    o.u.ew.mean, o.u.ew.std = m.data_ptr(), s.data_ptr()
+                self.ext_in.setdefault(op.key, []).append((len(self.fwd), op))
+                self.fwd.append(o)
+            elif isinstance(op, ConvOp):
+                lay, x, out = op.layer, op.x, op.out
+                ext = out.buf.external
+                o = self.conv_desc(
+                    self.ptr(x), x.buf.C, nf, x.H, x.W, x.c, lay.wf.data_ptr(), lay.kpad, lay.cout_p, out.H, out.W,
+                    lay.stride, lay.stride, lay.fwd_taps(), 0 if ext else self.ptr(out), out.buf.C, out.H, out.W,
+                    bias=lay.bias_p.data_ptr() if lay.has_bias else None,
+                    res=self.ptr(op.res) if op.res is not None else None,
+                    res_ld=op.res.buf.C if op.res is not None else 0, act=op.act,
+                    out_f32=(out.buf.dt == torch.float32 and self.dtype != torch.float32))
+                if ext:
+                    self.ext_out.setdefault(out.buf.name, []).append((len(self.fwd), out))
+                self.fwd.append(o)
+            elif isinstance(op, FuseOp):
+                out = op.out
+                srcs = [(self.ptr(s), s.buf.C, s.H, s.W) for s in op.srcs]
+                self.fwd.append(self.ew_desc(L.EW_FUSE, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C, srcs,
+                                             act=op.act))
+            elif isinstance(op, PoolOp):
+                x, out = op.x, op.out
+                self.fwd.append(self.ew_desc(L.EW_POOL, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C,
+                                             [(self.ptr(x), x.buf.C, x.H, x.W)]))
+            elif isinstance(op, L1FeatOp):
+                a = op.a
+                half = nf // 2
+                o = self._op(L.OP_LOSS)
+                d = o.u.loss
+                d.a, d.b = self.ptr(a, 0), self.ptr(a, half)
+                sn, sh, sw = a.H * a.W * a.buf.C, a.W * a.buf.C, a.buf.C
+                d.a_sn, d.a_sc, d.a_sh, d.a_sw = sn, 1, sh, sw
+                d.b_sn, d.b_sc, d.b_sh, d.b_sw = sn, 1, sh, sw
+                d.kind, d.bsz, d.ch, d.h, d.w, d.dtype = L.LOSS_L1NHWC, half, a.c, a.H, a.W, self.dt
+                d.weight = 1.0
+                npart = L.load().dvie_loss_partial_count(ctypes.byref(d))
+                part = torch.zeros(max(1, npart), dtype=torch.float64, device=self.device)
+                self.keep.append(part)
+                d.partial = part.data_ptr()
+                d.out = self.l1_out.data_ptr() + 4 * op.idx
+                self.fwd.append(o)
+            else:
+                raise TypeError(op)
+
+    # ---------------- backward ----------------
+    def _contrib(self, region, emitter, ident=None):
+        """Record a gradient contribution to `region`'s buffer: either a kernel
+        (emitter(beta, res_ptr, res_ld, dact, z_ptr, z_ld) -> ops) or an identity
+        (`ident` = (ptr, ld) of a gradient region with the same shape)."""
+        b = region.buf
+        assert region.key() == b.read_region
+        b.pending.append((emitter, ident))
+        if len(b.pending) == b.expected:
+            self._flush(b)
+
+    def _flush(self, b):
+        c0, c = b.read_region
+        region = Region(b, c0, c)
+        kernels = [e for e, i in b.pending if e is not None]
+        idents = [i for e, i in b.pending if e is None]
+        prod = b.producers
+        fuse_dact = (len(prod) == 1 and prod[0].act != L.ACT_NONE and prod[0].out.key() == b.read_region)
+        b.dact_done = fuse_dact
+        dact = prod[0].act if fuse_dact else 0
+        z = self.ptr(region) if fuse_dact else None
+        if fuse_dact:
+            assert b.dt == self.dtype
+        seq = []
+        k = 0
+        for em in kernels:
+            r = idents[k] if k < len(idents) else None
+            k += 1 if r is not None else 0
+            seq.append((em, r))
+        rest = idents[k:]
+        gptr, gld = self.ptr(region, grad=True), b.C
+        while rest:
+            a = rest.pop(0)
+            r = rest.pop(0) if rest else None
+
+            def copy_em(beta, res, res_ld, dact_, z_, z_ld_, a=a):
+                return [self.ew_desc(L.EW_COPY, self.nb, b.H, b.W, c, gptr, gld, [(a[0], a[1], b.H, b.W)],
+                                     res=res, res_ld=res_ld, z=z_, z_ld=z_ld_, dact=dact_, beta=beta)]
+
+            seq.append((copy_em, r))
+        for i, (em, r) in enumerate(seq):
+            last = i == len(seq) - 1
+            ops = em(0 if i == 0 else 1, r[0] if r else None, r[1] if r else 0, dact if last else 0,
+                     z if last else None, b.C if last else 0)
+            self.bwd.extend(ops)
+        b.done = True
+        b.pending = []
+
+    def _ensure_dact(self, op):
+        """Producer-side activation derivative when it could not be fused upstream."""
+        b = op.out.buf
+        if op.act == L.ACT_NONE or getattr(b, "dact_done", False):
+            return
+        out = op.out
+        gp = self.ptr(out, grad=True)
+        self.bwd.append(self.ew_desc(L.EW_COPY, self.nb, out.H, out.W, out.c, gp, b.C, [(gp, b.C, out.H, out.W)],
+                                     z=self.ptr(out), z_ld=b.C, dact=op.act))
+
+    def _build_backward(self):
+        g = self.g
+        nb = self.nb
+        self.wg_first = {}
+        for key, (region, ch) in g.outputs.items():
+            b = region.buf
+            assert b.needs_grad and b.expected == 0 and all(p.act == L.ACT_NONE for p in b.producers)
+            o = self.ew_desc(L.EW_NCHW, nb, region.H, region.W, region.c, self.ptr(region, grad=True), b.C)
+            o.u.ew.ext_c = ch
+            self.ext_ograd[key] = len(self.bwd)
+            self.bwd.append(o)
+            b.done = True
+            b.dact_done = True
+        for op in reversed(g.ops):
+            if isinstance(op, L1FeatOp):
+                a = op.a
+                if not a.buf.needs_grad:
+                    continue
+                numel = (self.nf // 2) * a.H * a.W * a.c
+                ap, bp, ld = self.ptr(a, 0), self.ptr(a, self.nf // 2), a.buf.C
+                gp = self.ptr(a, grad=True)
+                scale = op.weight / numel
+
+                def em(beta, res, res_ld, dact, z, z_ld, a=a, ap=ap, bp=bp, ld=ld, gp=gp, scale=scale):
+                    return [self.ew_desc(L.EW_L1SIGN, nb, a.H, a.W, a.c, gp, ld, [(ap, ld, a.H, a.W), (bp, ld, a.H, a.W)],
+                                         res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta, scale=scale)]
+
+                self._contrib(a, em)
+                continue
+            out = op.out
+            b = out.buf
+            if not b.needs_grad or not getattr(b, "done", False):
+                continue  # no gradient reaches this op
+            self._ensure_dact(op)
+            gout, gld = self.ptr(out, grad=True), b.C
+            if isinstance(op, InputOp):
+                if op.requires_grad:
+                    o = self.ew_desc(L.EW_TONCHW, nb, out.H, out.W, out.c, 0, 0, [(gout, gld, out.H, out.W)])
+                    o.u.ew.ext_c = op.ext_c
+                    self.ext_grad.setdefault(op.key, []).append((len(self.bwd), op))
+                    self.bwd.append(o)
+                continue
+            if isinstance(op, ConvOp):
+                self._conv_backward(op, gout, gld)
+            elif isinstance(op, FuseOp):
+                for s in op.srcs:
+                    if not s.buf.needs_grad:
+                        continue
+                    if (s.H, s.W) == (out.H, out.W):
+                        self._contrib(s, None, ident=(gout, gld))
+                    else:
+                        sp = self.ptr(s, grad=True)
+
+                        def em(beta, res, res_ld, dact, z, z_ld, s=s, sp=sp, out=out, gout=gout, gld=gld):
+                            return [self.ew_desc(L.EW_UPT, nb, s.H, s.W, s.c, sp, s.buf.C, [(gout, gld, out.H, out.W)],
+                                                 res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)]
+
+                        self._contrib(s, em)
+            elif isinstance(op, PoolOp):
+                x = op.x
+                if x.buf.needs_grad:
+                    xp = self.ptr(x, grad=True)
+
+                    def em(beta, res, res_ld, dact, z, z_ld, x=x, xp=xp, out=out, gout=gout, gld=gld):
+                        return [self.ew_desc(L.EW_POOLT, nb, x.H, x.W, x.c, xp, x.buf.C, [(gout, gld, out.H, out.W)],
+                                             res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)]
+
+                    self._contrib(x, em)
+        # (buffers whose contributions never completed would indicate a graph bug)
+        for bf in g.buffers:
+            if bf.needs_grad and bf.expected and not getattr(bf, "done", False):
+                raise RuntimeError(f"incomplete gradient for {bf}: {len(bf.pending)}/{bf.expected}")
+
+    def _conv_backward(self, op, gout, gld):
+        lay, x, out = op.layer, op.x, op.out
+        nb = self.nb
+        npix = nb * out.H * out.W
+        taps = lay.fwd_taps()
+        if lay.trainable:
+            # weight gradient: split-K partial slabs + reduction into the OIHW .grad view
+            tiles = rup(lay.cout_p, 64) // 64 * (rup(x.c, 64) // 64)
+            ntap = lay.kh * lay.kw
+            bkp = 64 if self.dtype == torch.bfloat16 else 32
+            splits = max(1, min(max(1, npix // (bkp * 4)), 2048 // max(1, tiles * ntap)))
+            o = self._op(L.OP_WGRAD)
+            d = o.u.wgrad
+            d.g, d.x, d.ws = gout, self.ptr(x), 0
+            d.g_ld, d.x_ld = gld, x.buf.C
+            d.n, d.oh, d.ow, d.cout = nb, out.H, out.W, lay.cout_p
+            d.ih, d.iw, d.c, d.sy, d.sx = x.H, x.W, x.c, lay.stride, lay.stride
+            d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], 1, 1
+            d.splits, d.dtype = splits, self.dt
+            self.ws_floats = max(self.ws_floats, splits * lay.cout_p * ntap * x.c)
+            self.bwd.append(o)
+            o = self._op(L.OP_WREDUCE)
+            r = o.u.wreduce
+            r.ws, r.dw, r.cinv = 0, 0, lay.cinv_t.data_ptr()
+            r.splits, r.ws_rows, r.ws_k, r.co_off = splits, lay.cout_p, ntap * x.c, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
+            first = lay not in self.wg_first
+            r.beta = 0 if first else 1
+            self.bwd.append(o)
+            self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
+            if lay.has_bias:
+                csplits = max(1, min(512, npix // 2048))
+                o = self._op(L.OP_COLSUM)
+                cd = o.u.colsum
+                cd.g, cd.ws, cd.g_ld, cd.rows, cd.c, cd.splits, cd.dtype = gout, 0, gld, npix, lay.cout_p, csplits, self.dt
+                self.ws_floats = max(self.ws_floats, csplits * lay.cout_p)
+                self.bwd.append(o)
+                o = self._op(L.OP_WREDUCE)
+                r = o.u.wreduce
+                r.ws, r.dw, r.cinv = 0, 0, None
+                r.splits, r.ws_rows, r.ws_k, r.co_off = csplits, lay.cout_p, 1, 0
+                r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
+                r.beta = 0 if first else 1
+                self.bwd.append(o)
+                self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
+            self.wg_first[lay] = True
+        if op.res is not None and op.res.buf.needs_grad:
+            self._contrib(op.res, None, ident=(gout, gld))
+        if x.buf.needs_grad:
+            phases = self._dgrad_weights(lay, x.H, x.W)
+            xg = self.ptr(x, grad=True)
+
+            def em(beta, res, res_ld, dact, z, z_ld, phases=phases, x=x, xg=xg, out=out, gout=gout, gld=gld, lay=lay):
+                ops = []
+                for ph, wt, kpad in phases:
+                    ops.append(self.conv_desc(
+                        gout, gld, nb, out.H, out.W, lay.cout_p, wt.data_ptr(), kpad, x.c, ph["oh"], ph["ow"], 1, 1,
+                        ph, xg, x.buf.C, x.H, x.W, osy=lay.stride, osx=lay.stride, ory=ph["ry"], orx=ph["rx"],
+                        res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta))
+                return ops
+
+            self._contrib(x, em)
+
+    # ---------------- finalize ----------------
+    def _finalize(self):
+        L.load()
+        # workspace for wgrad / colsum partials
+        self.ws = torch.empty(max(1, self.ws_floats), dtype=torch.float32, device=self.device)
+        self.keep.append(self.ws)
+        for o in self.bwd:
+            if o.kind == L.OP_WGRAD:
+                o.u.wgrad.ws = self.ws.data_ptr()
+            elif o.kind == L.OP_COLSUM:
+                o.u.colsum.ws = self.ws.data_ptr()
+            elif o.kind == L.OP_WREDUCE:
+                o.u.wreduce.ws = self.ws.data_ptr()
+        # pack op (all layers, one launch) goes first in the forward list
+        descs = self._pack_descs
+        arr = (L.PackDesc * len(descs))(*descs)
+        raw = bytes(arr)
+        dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self.keep.append(dev)
+        po = self._op(L.OP_PACK)
+        po.u.pack.descs_dev = dev.data_ptr()
+        po.u.pack.n = len(descs)
+        po.u.pack.max_elems = max(d.rows * d.kpad for d in descs)
+        self.fwd_arr = (L.Op * (len(self.fwd) + 1))(po, *self.fwd)
+        self.fwd_off = 1
+        self.bwd_arr = (L.Op * max(1, len(self.bwd)))(*self.bwd) if self.bwd else None
+        self.n_bwd = len(self.bwd)
+
+    # ---------------- execution ----------------
+    def set_input(self, key, t):
+        """Patch the external NCHW fp32 input `t` (any strides) into the forward list."""
+        assert t.dtype == torch.float32 and t.device.type == self.device.type
+        for idx, op in self.ext_in[key]:
+            d = self.fwd_arr[idx + self.fwd_off].u.ew
+            assert t.shape[0] == self._part(op.part)[1], (key, tuple(t.shape), self.nf)
+            assert t.shape[2:] == (op.out.H, op.out.W) and t.shape[1] >= op.ext_c0 + op.ext_c, (key, tuple(t.shape))
+            sn, sc, sh, sw = t.stride()
+            d.ext = t.data_ptr() + 4 * op.ext_c0 * sc
+            d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+
+    def set_output(self, name, t):
+        for idx, region in self.ext_out[name]:
+            d = self.fwd_arr[idx + self.fwd_off].u.conv
+            d.y = t.data_ptr() + region.c0 * t.element_size()
+            d.y_ld = t.shape[-1]
+
+    def set_output_grad(self, key, t):
+        """Patch the incoming gradient (fp32, any strides, logical NCHW) of output `key`."""
+        assert t.dtype == torch.float32
+        d = self.bwd_arr[self.ext_ograd[key]].u.ew
+        sn, sc, sh, sw = t.stride()
+        d.ext = t.data_ptr()
+        d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+
+    def set_input_grad(self, key, t, accumulate=False):
+        for idx, op in self.ext_grad[key]:
+            d = self.bwd_arr[idx].u.ew
+            sn, sc, sh, sw = t.stride()
+            d.ext = t.data_ptr() + 4 * op.ext_c0 * sc
+            d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+            d.beta = int(accumulate)
+
+    def set_param_grads(self, accumulate=False):
+        """Point weight reductions at the parameters' .grad tensors (fp32, OIHW)."""
+        for idx, lay, which, first in self._grad_slots:
+            p = getattr(lay.m, which)
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            d = self.bwd_arr[idx].u.wreduce
+            d.dw = p.grad.data_ptr()
+            if first:
+                d.beta = int(accumulate)
+
+    def run_forward(self, stream=None):
+        s = L.stream_ptr() if stream is None else stream
+        L.check(L.load().dvie_run_ops(ctypes.addressof(self.fwd_arr), len(self.fwd_arr), s), "forward plan")
+        self.generation += 1
+
+    def run_backward(self, stream=None):
+        if self.n_bwd == 0:
+            return
+        s = L.stream_ptr() if stream is None else stream
+        L.check(L.load().dvie_run_ops(ctypes.addressof(self.bwd_arr), self.n_bwd, s), "backward plan")
+
+    def zero_grad_buffers(self):
+        for b in self.g.buffers:
+            if b.g is not None:
+                b.g.zero_()
+
+    def describe(self):
+        kinds = {}
+        for o in list(self.fwd) + list(self.bwd):
+            kinds[o.kind] = kinds.get(o.kind, 0) + 1
+        return dict(n_fwd=len(self.fwd) + 1, n_bwd=self.n_bwd, kinds=kinds, ws_mb=self.ws_floats * 4 / 2**20)
+
+

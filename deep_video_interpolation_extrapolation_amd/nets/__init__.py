@@ -1,0 +1,6 @@
+"""Model factory: `nets.__dict__[name](args)` as in the reference (nets/__init__.py:1-33)."""
+from .conv import Conv2d
+from .ExtraNet import ExtraNet
+from .HRNet import HRNet
+from .InterNet import InterNet
+from .vgg import VGG19, my_vgg, vgg19_features

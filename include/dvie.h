@@ -1,0 +1,321 @@
+/*
+ * dvie.h — C ABI of the MI355X-native frame-synthesis hot path
+ * (deep_video_interpolation_extrapolation, HIP/CDNA4, gfx950).
+ *
+ * One shared library (libdvie.so) exports these entry points.  Every entry point takes
+ * raw device pointers, plain integer shapes/strides and a hipStream_t (passed as void*),
+ * launches asynchronously on that stream, never allocates, and returns an int status
+ * (DVIE_OK = 0, DVIE_EINVAL = argument validation failure, otherwise a hipError_t).
+ *
+ * Activations are NHWC ("channels_last"): element (n, y, x, c) of a tensor with pixel
+ * stride `ld` (elements) lives at base[((n*H + y)*W + x)*ld + c].  A channel slice of a
+ * wider buffer is addressed by offsetting `base` and keeping the wider `ld`.
+ *
+ * The reference has no native code: every entry point replaces a PyTorch/cuDNN op that
+ * the reference calls from Python.  The reference call site each one replaces is cited
+ * next to it (paths relative to the reference repository root).
+ */
+#ifndef DVIE_H
+#define DVIE_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVIE_OK 0
+#define DVIE_EINVAL 1001
+
+/* element types */
+#define DVIE_F32 0
+#define DVIE_BF16 1
+
+/* activations (forward) and activation derivatives (backward, computed from the
+ * activation's OUTPUT z: lrelu'(z) = z > 0 ? 1 : alpha, elu'(z) = z > 0 ? 1 : z + 1,
+ * relu'(z) = z > 0) */
+#define DVIE_ACT_NONE 0
+#define DVIE_ACT_LRELU 1 /* nn.LeakyReLU(0.2)  nets/HRNet.py:22,59,107 */
+#define DVIE_ACT_ELU 2   /* nn.ELU()           nets/HRNet.py:360,362    */
+#define DVIE_ACT_RELU 3  /* VGG19 ReLU         nets/vgg.py:11-54         */
+
+/*
+ * Implicit-GEMM convolution (forward, and data-gradient as a forward conv over the
+ * output gradient with re-packed weights).  Replaces nn.Conv2d forward/backward-data:
+ *   3x3 s1 / 3x3 s2 / 1x1 convs of nets/HRNet.py:9-12,52-57,127-129,166-194,367-371,
+ *   410-441,444-477; seg encoder nets/HRNet.py:358-364; VGG19 convs nets/vgg.py:11-54.
+ *
+ * GEMM view: rows = output channels (cout), columns = output pixels of the grid
+ * (n, oy, ox) in [0,n)x[0,oh)x[0,ow), reduction over K = taps * c:
+ *   acc[co][pix] = sum_{t,ci} w[co][t*c + ci] * x[n][oy*sy + dy(t)][ox*sx + dx(t)][ci]
+ * with taps on a th x tw grid, dy(i,j) = dy0 + i*ddy, dx(i,j) = dx0 + j*ddx and
+ * t = i*tw + j; out-of-image taps read zero.  w is packed [cout][kpad] (kpad a multiple
+ * of 64 elements, zero-filled past taps*c).
+ * The result for pixel (n,oy,ox) lands at output position
+ *   (n, oy*osy + ory, ox*osx + orx) of a yh x yw image with pixel stride y_ld,
+ * which is how the stride-2 data gradient writes its 4 phases.
+ * Epilogue, in order: v = acc; v += bias[co]; v += res; v += y_old (beta=1);
+ *   v = act(v) (forward activation); v *= act'(z) (dact, derivative from output z);
+ *   y = v.
+ * Constraints: c % (16/sizeof(elem)) == 0, cout % 4 == 0, every ld % 4 == 0, pointers
+ * 16-byte aligned for x/w and 8-byte aligned (bf16) / 16-byte (f32) for y/res/z.
+ */
+typedef struct dvie_conv_desc {
+  const void* x;
+  const void* w;
+  void* y;
+  const float* bias; /* [cout] fp32 or NULL */
+  const void* res;   /* residual at output placement or NULL (same elem type as y) */
+  const void* z;     /* activation output for dact (elem type = dtype) or NULL */
+  long long x_ld, y_ld, res_ld, z_ld;
+  int n, ih, iw, c;
+  int kpad, cout;
+  int oh, ow, sy, sx;
+  int th, tw, dy0, dx0, ddy, ddx;
+  int yh, yw, osy, osx, ory, orx;
+  int act, dact, beta, dtype;
+  int out_f32; /* 1: y (and res) are fp32, 0: y has elem type dtype */
+  float alpha; /* activation slope / parameter */
+} dvie_conv_desc;
+
+int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream);
+
+/*
+ * Weight gradient of the convolution above (replaces nn.Conv2d backward-weight):
+ *   part[s][co][t*c + ci] = sum_{pix in split s} g[pix][co] * x[pix + tap t][ci]
+ * g is the pre-activation output gradient on the (n, oh, ow) grid (pixel stride g_ld),
+ * x the forward input.  The pixel range is cut into `splits` contiguous chunks; fp32
+ * partials go to `ws` ([splits][cout][taps*c]).  dvie_wgrad_reduce then sums them.
+ */
+typedef struct dvie_wgrad_desc {
+  const void* g;
+  const void* x;
+  float* ws;
+  long long g_ld, x_ld;
+  int n, oh, ow, cout;
+  int ih, iw, c, sy;
+  int sx, th, tw, dy0;
+  int dx0, ddy, ddx, splits;
+  int dtype, pad0;
+} dvie_wgrad_desc;
+
+int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream);
+
+/*
+ * dw[co][ci][kh][kw] (+)= sum_s part[s][co][t*c + cpos]  for every (co, ci, kh, kw) of an
+ * OIHW fp32 parameter gradient, where cpos = cinv[ci] (position of source channel ci in
+ * the packed channel order, or ci itself when cinv is NULL) and t = kh*kw_n + kw.
+ * Also used for bias gradients (kh_n = kw_n = 1, cin = 1, taps*c = 1).
+ * `co_off` selects rows [co_off, co_off + cout_p) of the partials.
+ */
+typedef struct dvie_wreduce_desc {
+  const float* ws;
+  float* dw;
+  const int* cinv;
+  int splits, ws_rows, ws_k, co_off;
+  int cout_p, cin_p, kh_n, kw_n;
+  int c, beta;
+} dvie_wreduce_desc;
+
+int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream);
+
+/* Bias gradient partials: part[s][co] = sum_{pix in split s} g[pix][co]. */
+typedef struct dvie_colsum_desc {
+  const void* g;
+  float* ws;
+  long long g_ld;
+  long long rows;
+  int c, splits, dtype, pad0;
+} dvie_colsum_desc;
+
+int dvie_colsum(const dvie_colsum_desc* d, void* stream);
+
+/*
+ * Weight packing: fp32 OIHW parameter -> packed GEMM operand rows (elem type dtype).
+ * mode 0 (forward):   dst[r][t*c + j] = src[r][cmap[j]][kh(t)][kw(t)], r < cout_s
+ * mode 1 (transpose): dst[r][t*c + j] = src[j][cmap[r]][kh(t)][kw(t)], j < cout_s
+ * with kh(t) = kh0 + (t / tw)*dkh, kw(t) = kw0 + (t % tw)*dkw; entries whose source is
+ * out of range (cmap < 0, r/j past the source extent, k >= taps*c) are zero.
+ * `n` descriptors are processed by one launch (descs points to DEVICE memory).
+ */
+typedef struct dvie_pack_desc {
+  const float* src;
+  void* dst;
+  const int* cmap; /* device int array or NULL (identity) */
+  int rows, kpad, c, mode;
+  int th, tw, kh0, kw0;
+  int dkh, dkw, cout_s, cin_s;
+  int kh_s, kw_s, dtype, pad0;
+} dvie_pack_desc;
+
+int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, void* stream);
+
+/*
+ * Pointwise NHWC family (4 channels per thread).  op selects:
+ *  DVIE_EW_FUSE   y = act( sum_i up_i(src_i) ) — HighResolutionModule fuse sum
+ *                 (nets/HRNet.py:212-225) and the final bilinear upsample into the
+ *                 448-channel concat (nets/HRNet.py:576-582).  up_i is bilinear,
+ *                 align_corners=False, from (src_h, src_w) to (h, w), identity when equal.
+ *  DVIE_EW_UPT    y = up^T(src_0) — adjoint of the bilinear upsample (gather form,
+ *                 deterministic, no atomics); src_0 is the fine grid (src_h x src_w).
+ *  DVIE_EW_POOL   y = avgpool2x2(src_0) (nets/vgg.py:9 AvgPool2d(2,2)).
+ *  DVIE_EW_POOLT  y = adjoint of avgpool2x2 applied to src_0 (coarse grid).
+ *  DVIE_EW_COPY   y = src_0 (same grid).
+ *  DVIE_EW_L1SIGN y = scale * sign(src_0 - src_1) (VGG feature-L1 gradient, losses.py:178-179)
+ *  DVIE_EW_NCHW   y = ext (fp32, arbitrary NCHW strides sn,sc,sh,sw; channels >= ext_c
+ *                 read as zero), optionally (ext - mean[c]) / std[c]
+ *                 (preprocess_norm, utils/net_utils.py:11-23).
+ *  DVIE_EW_TONCHW ext (+)= channels [0, ext_c) of src_0 as fp32 with NCHW strides
+ *                 (beta selects accumulate; the NHWC epilogue is not applied).
+ * then the shared epilogue: v += res; v += y_old (beta); v = act(v); v *= act'(z); y = v.
+ * Channels c % 4 == 0; all lds % 4 == 0.
+ */
+#define DVIE_EW_FUSE 0
+#define DVIE_EW_UPT 1
+#define DVIE_EW_POOL 2
+#define DVIE_EW_POOLT 3
+#define DVIE_EW_COPY 4
+#define DVIE_EW_L1SIGN 5
+#define DVIE_EW_NCHW 6
+#define DVIE_EW_TONCHW 7
+
+typedef struct dvie_ew_desc {
+  void* y;
+  const void* src0;
+  const void* src1;
+  const void* src2;
+  const void* res;
+  const void* z;
+  float* ext;
+  const float* mean;
+  const float* std;
+  long long y_ld, src_ld0, src_ld1, src_ld2, res_ld, z_ld;
+  long long sn, sc, sh, sw;
+  int op, n, h, w;
+  int c, nsrc, sh0, sw0;
+  int sh1, sw1, sh2, sw2;
+  int act, dact, beta, dtype;
+  int ext_c, pad0;
+  float alpha, scale;
+} dvie_ew_desc;
+
+int dvie_ew(const dvie_ew_desc* d, void* stream);
+
+/*
+ * Loss reductions on fp32 NCHW-strided (B, C, H, W) images (pred a, target b).
+ * Every loss writes its partial sums to `partial` (double[nblocks]) and the final
+ * scalar (fp32) to `out`, and — when `grad` is non-NULL — the gradient of `weight *
+ * loss` with respect to a in NCHW-contiguous fp32 layout ([B][C][H][W]), overwritten
+ * (beta=0) or accumulated (beta=1).
+ *  L1   : mean|a-b|                                   nn.L1Loss (losses.py:224)
+ *  GDL  : (mean|dx a - dx b| + mean|dy a - dy b|)/2   GDLLoss (losses.py:137-151)
+ *  SSIM : 1 - mean ssim_map (11x11 gaussian, sigma 1.5, zero pad 5, C1=1e-4, C2=9e-4)
+ *                                                      SSIM/_ssim (losses.py:18-48,63-87)
+ *  MSE  : per-sample mean((a-b)^2) -> out[b] (PSNR, losses.py:103-116)
+ *  CE   : mean_pix( logsumexp(a[:,.]) - a[label] ), label = argmax_c b[:, c]
+ *         (nn.CrossEntropyLoss(a, argmax(b,1)), runners/InterTrainer.py:75,414)
+ */
+#define DVIE_LOSS_L1 0
+#define DVIE_LOSS_GDL 1
+#define DVIE_LOSS_SSIM 2
+#define DVIE_LOSS_MSE 3
+#define DVIE_LOSS_CE 4
+#define DVIE_LOSS_L1NHWC 5 /* mean|a-b| over NHWC tensors of elem type dtype (VGG features) */
+
+typedef struct dvie_loss_desc {
+  const void* a;
+  const void* b;
+  float* grad;
+  float* out;
+  double* partial;
+  float* ws; /* SSIM gradient scratch: 3*B*C*H*W floats (dvie_loss_ws_floats) */
+  long long a_sn, a_sc, a_sh, a_sw;
+  long long b_sn, b_sc, b_sh, b_sw;
+  int kind, bsz, ch, h;
+  int w, beta, dtype, pad0;
+  float weight, pad1;
+} dvie_loss_desc;
+
+int dvie_loss(const dvie_loss_desc* d, void* stream);
+size_t dvie_loss_partial_count(const dvie_loss_desc* d);
+size_t dvie_loss_ws_floats(const dvie_loss_desc* d);
+
+/*
+ * Bilinear flow warp (FlowWrapper, utils/net_utils.py:89-114; F.grid_sample bilinear,
+ * zeros padding, align_corners=True as in the pinned torch 1.0.1):
+ *   gx = linspace(-1,1,W)[x] - flow[n,0,y,x],  gy = linspace(-1,1,H)[y] - flow[n,1,y,x]
+ *   out[n,c,y,x] = bilinear(img[n,c], (gx+1)/2*(W-1), (gy+1)/2*(H-1))
+ * fp32, NCHW contiguous.  Backward: dimg (accumulated with atomics — zero it first) and
+ * dflow (overwritten), given dout.
+ */
+typedef struct dvie_warp_desc {
+  const float* img;
+  const float* flow;
+  float* out;
+  const float* dout;
+  float* dimg;
+  float* dflow;
+  int n, c, h, w;
+  int align_corners, pad0;
+} dvie_warp_desc;
+
+int dvie_warp_fwd(const dvie_warp_desc* d, void* stream);
+int dvie_warp_bwd(const dvie_warp_desc* d, void* stream);
+
+/*
+ * Fused Adamax step over a flat fp32 buffer (torch.optim.Adamax semantics,
+ * runners/InterTrainer.py:79): m = lerp(m, g, 1-b1); u = max(u*b2, |g|+eps);
+ * p -= clr * m / u with clr = lr / (1 - b1^step) (computed by the caller);
+ * weight decay applied as g += wd*p first.
+ */
+int dvie_adamax(float* p, const float* g, float* m, float* u, long long n, float clr,
+                float b1, float b2, float eps, float wd, void* stream);
+
+/* scale a flat fp32 buffer in place (used for the 1/W gradient factor) */
+int dvie_scale(float* p, long long n, float s, void* stream);
+
+/*
+ * Op-list executor: runs n descriptors in order on one stream with a single host call
+ * (the per-step forward and backward plans of the HRNet / VGG executors).
+ */
+#define DVIE_OP_CONV 1
+#define DVIE_OP_WGRAD 2
+#define DVIE_OP_WREDUCE 3
+#define DVIE_OP_COLSUM 4
+#define DVIE_OP_EW 5
+#define DVIE_OP_LOSS 6
+#define DVIE_OP_PACK 7
+
+typedef struct dvie_pack_list {
+  const dvie_pack_desc* descs_dev;
+  int n, max_elems;
+} dvie_pack_list;
+
+typedef struct dvie_op {
+  int kind;
+  int pad0;
+  union {
+    dvie_conv_desc conv;
+    dvie_wgrad_desc wgrad;
+    dvie_wreduce_desc wreduce;
+    dvie_colsum_desc colsum;
+    dvie_ew_desc ew;
+    dvie_loss_desc loss;
+    dvie_pack_list pack;
+  } u;
+} dvie_op;
+
+int dvie_run_ops(const dvie_op* ops, int n, void* stream);
+
+/* ABI self-check: sizeof of each descriptor, indexed by DVIE_OP_* (0 = dvie_op). */
+size_t dvie_abi_sizeof(int which);
+/* library version string */
+const char* dvie_version(void);
+/* last error text of the calling thread (argument validation) */
+const char* dvie_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DVIE_H */

@@ -1,0 +1,62 @@
+"""Oracle: one InterTrainer training step (reference runners/InterTrainer.py:380-441).
+
+  gt_x = frame2; x = cat(frame1, frame3); seg = cat(seg1, seg3)
+  coarse_img, coarse_seg = InterNet(x, seg)                  (nets/InterNet.py:14-17)
+  loss_dict = RGBLoss(coarse_img, gt_x, normed=False)        (losses.py:223-241)
+  loss_dict['coarse_ce_loss'] = 30 * CE(coarse_seg, argmax(gt_seg))
+  loss_all = sum(mean(v)); sync (value mean over ranks, gradient scaled by 1/W)
+  zero_grad; backward; Adamax(lr=1e-3).step()                (l.79, l.427-437)
+"""
+from collections import OrderedDict
+
+import torch
+
+from . import hrnet, losses
+
+
+def synthetic_batch(n, H, W, first_index=0):
+    """Synthetic Cityscapes-shaped triplets: sample i seeded 1000+i,
+    frames rand*2-1 (3,H,W), segs one-hot of randint(0,20) (20,H,W)."""
+    out = {f"frame{k}": [] for k in (1, 2, 3)}
+    out.update({f"seg{k}": [] for k in (1, 2, 3)})
+    for i in range(first_index, first_index + n):
+        g = torch.Generator().manual_seed(1000 + i)
+        for k in (1, 2, 3):
+            out[f"frame{k}"].append(torch.rand((3, H, W), generator=g) * 2 - 1)
+        for k in (1, 2, 3):
+            lab = torch.randint(0, 20, (H, W), generator=g)
+            out[f"seg{k}"].append(torch.nn.functional.one_hot(lab, 20).permute(2, 0, 1).float())
+    return {k: torch.stack(v) for k, v in out.items()}
+
+
+def inter_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(80.0, 80.0, 20.0, 20.0, 30.0)):
+    """Returns (loss_dict values, grads dict, updated params, adamax state)."""
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+    gt_x, gt_seg = data["frame2"], data["seg2"]
+    x = torch.cat([data["frame1"], data["frame3"]], 1)
+    seg = torch.cat([data["seg1"], data["seg3"]], 1)
+    rgb, seg_out = hrnet.forward(P, torch.cat([x, seg], 1))
+    ld = losses.rgb_loss(vgg_state, rgb, gt_x, normed=False, w=weights[:4])
+    ld["coarse_ce_loss"] = weights[4] * losses.seg_ce(seg_out, gt_seg)
+    loss = 0
+    for v in ld.values():
+        loss = loss + torch.mean(v)
+    ld["loss_all"] = loss
+    (loss / world).backward()
+    grads = {k: v.grad.detach().clone() for k, v in P.items()}
+    new, state = adamax(params, grads, lr, state)
+    return OrderedDict((k, float(v)) for k, v in ld.items()), grads, new, state, (rgb.detach(), seg_out.detach())
+
+
+def adamax(params, grads, lr, state=None, betas=(0.9, 0.999), eps=1e-8):
+    """torch.optim.Adamax update (the reference optimizer, InterTrainer.py:79)."""
+    state = state or {k: dict(step=0, exp_avg=torch.zeros_like(v), exp_inf=torch.zeros_like(v)) for k, v in params.items()}
+    new = {}
+    for k, p in params.items():
+        s, g = state[k], grads[k]
+        s["step"] += 1
+        s["exp_avg"] = s["exp_avg"].lerp(g, 1 - betas[0])
+        s["exp_inf"] = torch.maximum(s["exp_inf"] * betas[1], g.abs() + eps)
+        clr = lr / (1 - betas[0] ** s["step"])
+        new[k] = p - clr * (s["exp_avg"] / s["exp_inf"])
+    return new, state

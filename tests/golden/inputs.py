@@ -1,0 +1,69 @@
+"""Seeded inputs of the golden fixtures (shared by make_golden.py and the tests)."""
+import torch
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def onehot(lab, n=20):
+    return torch.nn.functional.one_hot(lab, n).permute(0, 3, 1, 2).float()
+
+
+def hrnet_input(n, H, W, seed=7):
+    g = _gen(seed)
+    x = torch.rand((n, 6, H, W), generator=g) * 2 - 1
+    seg = torch.cat([onehot(torch.randint(0, 20, (n, H, W), generator=g)) for _ in range(2)], 1)
+    return x, seg
+
+
+def rgbloss_inputs():
+    g = _gen(11)
+    pred = torch.rand((2, 3, 16, 32), generator=g) * 2 - 1
+    gt = (torch.rand((2, 3, 16, 32), generator=g) * 2 - 1) * 0.7 + 0.2 * pred
+    g01 = _gen(12)
+    p01 = torch.rand((2, 3, 16, 32), generator=g01)
+    t01 = torch.rand((2, 3, 16, 32), generator=g01) * 0.6 + 0.3 * p01
+    return {"pm1": (pred, gt, False), "z1": (p01, t01, False), "normed": (pred, gt, True)}
+
+
+def ce_inputs():
+    g = _gen(13)
+    logits = torch.randn((2, 20, 16, 32), generator=g) * 3
+    lab = torch.randint(0, 20, (2, 16, 32), generator=g)
+    return logits, onehot(lab)
+
+
+def warp_inputs():
+    g = _gen(17)
+    x = torch.rand((2, 3, 16, 20), generator=g)
+    flow = (torch.rand((2, 2, 16, 20), generator=g) * 2 - 1) * 0.6  # reaches outside the image
+    dout = torch.randn((2, 3, 16, 20), generator=g)
+    return x, flow, dout
+
+
+def metric_inputs():
+    g = _gen(19)
+    pred = torch.rand((2, 3, 32, 64), generator=g)
+    gt = (pred + 0.1 * torch.randn((2, 3, 32, 64), generator=g)).clamp(0, 1)
+    return pred, gt
+
+
+def iou_inputs():
+    g = _gen(23)
+    a = torch.randint(0, 20, (2, 32, 64), generator=g)
+    b = torch.where(torch.rand((2, 32, 64), generator=g) < 0.7, a, torch.randint(0, 20, (2, 32, 64), generator=g))
+    return a, b
+
+
+def step_batch(n, H, W):
+    out = {f"frame{k}": [] for k in (1, 2, 3)}
+    out.update({f"seg{k}": [] for k in (1, 2, 3)})
+    for i in range(n):
+        g = _gen(1000 + i)
+        for k in (1, 2, 3):
+            out[f"frame{k}"].append(torch.rand((3, H, W), generator=g) * 2 - 1)
+        for k in (1, 2, 3):
+            lab = torch.randint(0, 20, (H, W), generator=g)
+            out[f"seg{k}"].append(torch.nn.functional.one_hot(lab, 20).permute(2, 0, 1).float())
+    return {k: torch.stack(v) for k, v in out.items()}

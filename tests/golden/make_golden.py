@@ -1,0 +1,146 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE code.
+
+Run in the build container (it needs /root/reference; the GPU box does not have it):
+    python tests/golden/make_golden.py
+It imports the reference's own modules (nets, losses, utils.net_utils) read-only with the
+offline stubs of ref_stubs.py and records their outputs on seeded inputs.  The fixtures are
+data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs stored).
+
+  hrnet_fwd.npz  G1: reference InterNet/HRNet forward, seed 1024, input (2,46,16,32)
+                     + per-parameter checksums of the seeded initial weights
+  rgbloss.npz    G2: reference RGBLoss components (+ d/dpred) on [-1,1] (normed=False,
+                     as InterTrainer calls it) and [0,1] inputs; CE
+  warp.npz       G3: reference FlowWrapper forward/backward (align_corners=True)
+  metrics.npz    G5: reference PSNR / SSIM / IoU / VGGCosineLoss
+  step.npz       G4: one training step of the reference modules (InterTrainer.py:380-441
+                     body): loss dict, per-parameter gradient stats, post-Adamax checksums
+"""
+import os
+import sys
+import types
+import warnings
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+warnings.filterwarnings("ignore")
+
+import inputs  # noqa: E402
+import ref_stubs  # noqa: E402
+from oracle.losses import synthetic_vgg19_state  # noqa: E402
+
+ref_stubs.install(synthetic_vgg19_state)
+import losses as ref_losses  # noqa: E402  (reference losses.py)
+import nets as ref_nets  # noqa: E402      (reference nets/)
+from utils import net_utils as ref_nu  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def args_ns(**kw):
+    a = types.SimpleNamespace(syn_type="inter", highres_large=False, coarse_model="HRNet", num_pred_once=1,
+                              inpaint=False, inpaint_mask=False, fix_init_frames=False, l1_weight=80.0,
+                              gdl_weight=80.0, vgg_weight=20.0, ssim_weight=20.0, ce_weight=30.0, vid_length=1)
+    a.__dict__.update(kw)
+    return a
+
+
+def checksums(sd):
+    names = sorted(sd)
+    return names, np.array([[float(sd[n].double().sum()), float((sd[n].double() ** 2).sum())] for n in names])
+
+
+def g1():
+    torch.manual_seed(1024)
+    model = ref_nets.InterNet(args_ns())
+    x, seg = inputs.hrnet_input(2, 16, 32)
+    with torch.no_grad():
+        rgb, segout = model(x, seg=seg)
+    names, cs = checksums(model.coarse_model.state_dict())
+    np.savez_compressed(os.path.join(HERE, "hrnet_fwd.npz"), rgb=rgb.numpy(), seg=segout.numpy(),
+                        param_names=np.array(names), param_checksums=cs,
+                        n_params=sum(p.numel() for p in model.parameters()))
+
+
+def g2():
+    out = {}
+    for tag, (pred, gt, normed) in inputs.rgbloss_inputs().items():
+        loss = ref_losses.RGBLoss(args_ns())
+        pred = pred.clone().requires_grad_(True)
+        d = loss(pred, gt, normed, prefix="coarse")
+        for k, v in d.items():
+            (g,) = torch.autograd.grad(v, pred, retain_graph=True)
+            key = k.replace("coarse_", "")
+            out[f"{tag}_{key}"] = np.float64(v.item())
+            out[f"{tag}_{key}_grad"] = g.numpy()
+    logits, onehot = inputs.ce_inputs()
+    logits = logits.clone().requires_grad_(True)
+    ce = torch.nn.CrossEntropyLoss()(logits, torch.argmax(onehot, dim=1))
+    (g,) = torch.autograd.grad(ce, logits)
+    out["ce"] = np.float64(ce.item())
+    out["ce_grad"] = g.numpy()
+    np.savez_compressed(os.path.join(HERE, "rgbloss.npz"), **out)
+
+
+def g3():
+    x, flow, dout = inputs.warp_inputs()
+    x = x.clone().requires_grad_(True)
+    flow = flow.clone().requires_grad_(True)
+    y = ref_nu.FlowWrapper()(x, flow)
+    gx, gf = torch.autograd.grad(y, (x, flow), dout)
+    np.savez_compressed(os.path.join(HERE, "warp.npz"), out=y.detach().numpy(), dx=gx.numpy(), dflow=gf.numpy())
+
+
+def g5():
+    pred, gt = inputs.metric_inputs()
+    psnr = ref_losses.PSNR()(pred, gt)
+    ssim = ref_losses.SSIM()(pred, gt)
+    a, b = inputs.iou_inputs()
+    iou = ref_losses.IoU()(a, b)
+    vcos = ref_losses.VGGCosineLoss()(pred * 2 - 1, gt * 2 - 1, normed=False)
+    np.savez_compressed(os.path.join(HERE, "metrics.npz"), psnr=psnr.item(), ssim=ssim.item(), iou=iou.item(),
+                        vgg_cos=vcos.item())
+
+
+def g4():
+    args = args_ns()
+    torch.manual_seed(1024)
+    model = ref_nets.InterNet(args)
+    rgb_loss = ref_losses.RGBLoss(args)
+    ce = torch.nn.CrossEntropyLoss()
+    opt = torch.optim.Adamax(list(model.coarse_model.parameters()), lr=1e-3)
+    data = inputs.step_batch(2, 32, 64)
+    # runners/InterTrainer.py:389-437 (W = 1: sync is the identity)
+    gt_x = data["frame2"]
+    gt_seg = data["seg2"]
+    x = torch.cat([data["frame1"], data["frame3"]], dim=1)
+    seg = torch.cat([data["seg1"], data["seg3"]], dim=1)
+    coarse_img, coarse_seg = model(x, seg=seg)
+    loss_dict = rgb_loss(coarse_img, gt_x, False, prefix="coarse")
+    loss_dict["coarse_ce_loss"] = args.ce_weight * ce(coarse_seg, torch.argmax(gt_seg, dim=1))
+    loss = 0
+    for v in loss_dict.values():
+        loss += torch.mean(v)
+    loss_dict["loss_all"] = loss
+    opt.zero_grad()
+    loss_dict["loss_all"].backward()
+    named = dict(model.coarse_model.named_parameters())
+    names = sorted(named)
+    gstats = np.array([[float(named[n].grad.double().sum()), float((named[n].grad.double() ** 2).sum()),
+                        float(named[n].grad.abs().max())] for n in names])
+    opt.step()
+    _, post = checksums({n: p.detach() for n, p in named.items()})
+    np.savez_compressed(os.path.join(HERE, "step.npz"), loss_names=np.array(list(loss_dict.keys())),
+                        loss_values=np.array([float(v) for v in loss_dict.values()]), param_names=np.array(names),
+                        grad_stats=gstats, post_checksums=post, rgb=coarse_img.detach().numpy()[:, :, ::4, ::4],
+                        seg=coarse_seg.detach().numpy()[:, :, ::4, ::4])
+
+
+if __name__ == "__main__":
+    for f in (g1, g2, g3, g5, g4):
+        f()
+        print("wrote", f.__name__)

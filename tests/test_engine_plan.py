@@ -1,0 +1,85 @@
+"""Plan compiler checks on CPU (descriptor lists are built; nothing is launched)."""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from deep_video_interpolation_extrapolation_amd import _lib as L
+from deep_video_interpolation_extrapolation_amd import engine as E
+from deep_video_interpolation_extrapolation_amd import nets
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def make(**kw):
+    a = types.SimpleNamespace(syn_type="inter", highres_large=False, coarse_model="HRNet")
+    a.__dict__.update(kw)
+    torch.manual_seed(1024)
+    return nets.InterNet(a)
+
+
+def test_param_names_and_seeded_init_match_reference():
+    f = np.load(os.path.join(G, "hrnet_fwd.npz"))
+    m = make()
+    sd = m.coarse_model.state_dict()
+    names = [str(n) for n in f["param_names"]]
+    assert sorted(sd) == names
+    cs = np.array([[float(sd[n].double().sum()), float((sd[n].double() ** 2).sum())] for n in names])
+    np.testing.assert_allclose(cs, f["param_checksums"], rtol=1e-12, atol=1e-12)
+    assert sum(p.numel() for p in m.parameters()) == int(f["n_params"])
+
+
+def test_params_are_views_of_one_flat_buffer():
+    hr = make().coarse_model
+    base = hr._flat.data_ptr()
+    end = base + hr._flat.numel() * 4
+    for p in hr.parameters():
+        assert base <= p.data_ptr() < end
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_hrnet_plan_structure(dtype):
+    hr = make().coarse_model
+    g = hr._lower(E.Graph(dtype), 32, 64)
+    plan = g.compile(2, torch.device("cpu"), backward=True)
+    kinds = plan.describe()["kinds"]
+    n_conv_fwd = sum(1 for op in g.ops if isinstance(op, E.ConvOp))
+    assert n_conv_fwd == 77
+    # every trainable conv gets one wgrad; stride-2 dgrads split into 4 phases
+    assert kinds[L.OP_WGRAD] == 77
+    n_s2 = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2)
+    n_dgrad = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.x.buf.needs_grad)
+    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2
+    # every buffer that needs a gradient received all of its contributions
+    for b in g.buffers:
+        if b.needs_grad and b.expected:
+            assert b.done
+
+
+def test_highres_large_builds():
+    hr = make(highres_large=True).coarse_model
+    g = hr._lower(E.Graph(torch.float32), 32, 64)
+    plan = g.compile(1, torch.device("cpu"), backward=True)
+    assert plan.describe()["n_bwd"] > 0
+
+
+def test_vgg_plan_structure():
+    from deep_video_interpolation_extrapolation_amd.nets.vgg import my_vgg, vgg19_features
+    v = my_vgg(vgg19_features())
+    g = E.Graph(torch.float32)
+    v.lower(g, 32, 64, normalize=True, loss=True)
+    plan = g.compile(4, torch.device("cpu"), n_bwd=2, backward=True)
+    k = plan.describe()["kinds"]
+    assert L.OP_WGRAD not in k  # frozen
+    assert g.n_l1 == 5
+
+
+def test_vgg_synthetic_weights_match_oracle():
+    from deep_video_interpolation_extrapolation_amd.nets.vgg import synthetic_vgg19_state as a
+    from oracle.losses import synthetic_vgg19_state as b
+    sa, sb = a(), b()
+    assert sa.keys() == sb.keys()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k])

@@ -1,0 +1,183 @@
+"""GPU parity: every HIP kernel family against the CPU oracle / plain fp32 PyTorch CPU.
+
+Tolerances (written per test): fp32 parity mode — the north-star bar, 1e-3 max-abs on
+network outputs (HRNet rgb/seg), tighter on single ops; bf16 mode — relative checks
+(bf16 has 8 significant bits).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import inputs
+from oracle import hrnet as O
+from oracle import losses as OL
+from oracle import warp as OW
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / max(1e-12, float(b.abs().max())))
+
+
+CONV_CASES = [
+    # cin, cout, k, stride, H, W, bias
+    (3, 64, 3, 1, 16, 24, True),
+    (64, 64, 3, 1, 32, 48, False),
+    (64, 128, 3, 2, 32, 48, False),
+    (128, 64, 1, 1, 16, 24, False),
+    (256, 128, 3, 2, 17, 23, False),
+    (448, 3, 3, 1, 16, 16, True),
+    (20, 32, 3, 1, 16, 16, True),
+    (32, 4, 3, 1, 16, 16, True),
+    (448, 448, 1, 1, 8, 16, True),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_conv2d_fwd_bwd(dev, case, prec, monkeypatch):
+    monkeypatch.setenv("DVIE_PRECISION", prec)
+    from deep_video_interpolation_extrapolation_amd.nets.conv import Conv2d
+    cin, cout, k, s, H, W, bias = case
+    torch.manual_seed(0)
+    m = Conv2d(cin, cout, k, s, k // 2, bias=bias)
+    x = torch.randn(2, cin, H, W)
+    ref = torch.nn.Conv2d(cin, cout, k, s, k // 2, bias=bias)
+    ref.load_state_dict(m.state_dict())
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    gy = torch.randn_like(yr)
+    yr.backward(gy)
+    m = m.to(dev)
+    xg = x.to(dev).requires_grad_(True)
+    y = m(xg)
+    y.backward(gy.to(dev))
+    torch.cuda.synchronize()
+    tol = 2e-5 if prec == "fp32" else 2e-2
+    assert rel_err(y, yr) < tol, ("fwd", rel_err(y, yr))
+    assert rel_err(xg.grad, xr.grad) < tol * 2, ("dgrad", rel_err(xg.grad, xr.grad))
+    assert rel_err(m.weight.grad, ref.weight.grad) < tol * 2, ("wgrad", rel_err(m.weight.grad, ref.weight.grad))
+    if bias:
+        assert rel_err(m.bias.grad, ref.bias.grad) < tol * 2
+
+
+def _loss_pair(dev, fn_dvie, fn_ref, a, b):
+    ag = a.to(dev).requires_grad_(True)
+    v = fn_dvie(ag, b.to(dev))
+    v.backward()
+    ar = a.clone().requires_grad_(True)
+    vr = fn_ref(ar, b)
+    vr.backward()
+    return float(v), float(vr), ag.grad.cpu(), ar.grad
+
+
+@pytest.mark.parametrize("name", ["l1", "gdl", "ssim"])
+def test_pixel_losses(dev, name):
+    from deep_video_interpolation_extrapolation_amd import losses as DL
+    fd = {"l1": DL.l1_loss, "gdl": DL.gdl_loss, "ssim": DL.ssim_loss}[name]
+    fr = {"l1": OL.l1_loss, "gdl": OL.gdl_loss, "ssim": OL.ssim_loss}[name]
+    pred, gt, _ = inputs.rgbloss_inputs()["pm1"]
+    v, vr, g, gr = _loss_pair(dev, fd, fr, pred, gt)
+    assert abs(v - vr) <= 1e-5 * max(1, abs(vr))
+    assert rel_err(g, gr) < 1e-4
+    # strided (channels-last) prediction, as HRNet outputs it
+    p2 = pred.permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
+    v2, _, g2, _ = _loss_pair(dev, fd, fr, p2, gt)
+    assert abs(v2 - vr) <= 1e-5 * max(1, abs(vr)) and rel_err(g2, gr) < 1e-4
+
+
+def test_cross_entropy(dev):
+    from deep_video_interpolation_extrapolation_amd import losses as DL
+    logits, onehot = inputs.ce_inputs()
+    v, vr, g, gr = _loss_pair(dev, DL.seg_cross_entropy, OL.seg_ce, logits, onehot)
+    assert abs(v - vr) < 1e-5
+    assert rel_err(g, gr) < 1e-5
+
+
+def test_psnr(dev):
+    from deep_video_interpolation_extrapolation_amd import losses as DL
+    pred, gt = inputs.metric_inputs()
+    assert abs(float(DL.PSNR()(pred.to(dev), gt.to(dev))) - float(OL.psnr(pred, gt))) < 1e-4
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_vgg_loss(dev, prec, monkeypatch):
+    monkeypatch.setenv("DVIE_PRECISION", prec)
+    from deep_video_interpolation_extrapolation_amd import losses as DL
+    pred, gt, _ = inputs.rgbloss_inputs()["pm1"]
+    vl = DL.VGGLoss().to(dev)
+    st = OL.synthetic_vgg19_state()
+    v, vr, g, gr = _loss_pair(dev, lambda a, b: vl(a, b, normed=False),
+                              lambda a, b: OL.vgg_loss(st, a, b, normed=False), pred, gt)
+    tol = 1e-4 if prec == "fp32" else 3e-2
+    assert abs(v - vr) <= tol * abs(vr)
+    assert rel_err(g, gr) < (1e-3 if prec == "fp32" else 1e-1)
+
+
+def test_warp(dev):
+    from deep_video_interpolation_extrapolation_amd.utils.net_utils import FlowWrapper
+    x, flow, dout = inputs.warp_inputs()
+    xg, fg = x.to(dev).requires_grad_(True), flow.to(dev).requires_grad_(True)
+    y = FlowWrapper()(xg, fg)
+    y.backward(dout.to(dev))
+    xr, fr = x.clone().requires_grad_(True), flow.clone().requires_grad_(True)
+    yr = OW.flow_warp(xr, fr)
+    yr.backward(dout)
+    assert float((y.cpu() - yr).abs().max()) < 1e-5
+    assert float((xg.grad.cpu() - xr.grad).abs().max()) < 1e-4
+    assert float((fg.grad.cpu() - fr.grad).abs().max()) < 1e-3
+
+
+def _hrnet(dev, prec, monkeypatch):
+    monkeypatch.setenv("DVIE_PRECISION", prec)
+    import types
+    from deep_video_interpolation_extrapolation_amd import nets
+    torch.manual_seed(1024)
+    m = nets.InterNet(types.SimpleNamespace(syn_type="inter", highres_large=False, coarse_model="HRNet"))
+    return m.to(dev)
+
+
+def test_hrnet_forward_fp32_parity(dev, monkeypatch):
+    """north-star bar: outputs within 1e-3 max-abs of the CPU reference on fixed seeds."""
+    m = _hrnet(dev, "fp32", monkeypatch)
+    P = O.init_params(1024)
+    x, seg = inputs.hrnet_input(2, 32, 64)
+    with torch.no_grad():
+        rgb, s = m(x.to(dev), seg.to(dev))
+        rr, sr = O.forward(P, torch.cat([x, seg], 1))
+    assert float((rgb.cpu() - rr).abs().max()) < 1e-3
+    assert float((s.cpu() - sr).abs().max()) < 1e-3
+
+
+def test_hrnet_backward_fp32_parity(dev, monkeypatch):
+    m = _hrnet(dev, "fp32", monkeypatch)
+    P = {k: v.clone().requires_grad_(True) for k, v in O.init_params(1024).items()}
+    x, seg = inputs.hrnet_input(2, 32, 64)
+    g = torch.Generator().manual_seed(5)
+    w1 = torch.randn((2, 3, 32, 64), generator=g)
+    w2 = torch.randn((2, 20, 32, 64), generator=g)
+    rgb, s = m(x.to(dev), seg.to(dev))
+    ((rgb * w1.to(dev)).sum() + (s * w2.to(dev)).sum()).backward()
+    rr, sr = O.forward(P, torch.cat([x, seg], 1))
+    ((rr * w1).sum() + (sr * w2).sum()).backward()
+    named = dict(m.coarse_model.named_parameters())
+    worst = 0.0
+    for k, p in P.items():
+        e = rel_err(named[k].grad, p.grad)
+        worst = max(worst, e)
+        assert e < 2e-3, (k, e)
+    print("worst relative grad error", worst)
+
+
+def test_hrnet_bf16_close_to_fp32(dev, monkeypatch):
+    m = _hrnet(dev, "bf16", monkeypatch)
+    P = O.init_params(1024)
+    x, seg = inputs.hrnet_input(2, 32, 64)
+    with torch.no_grad():
+        rgb, s = m(x.to(dev), seg.to(dev))
+        rr, sr = O.forward(P, torch.cat([x, seg], 1))
+    assert torch.isfinite(rgb).all() and torch.isfinite(s).all()
+    assert rel_err(rgb, rr) < 5e-2 and rel_err(s, sr) < 5e-2
