@@ -1,0 +1,179 @@
+"""Throughput benchmark: InterNet (HRNet) training steps on synthetic 256x512 len-3 clips.
+
+    python bench.py [--gpus N --steps K --warmup W]            (N>1: launched by torchrun)
+
+Workload (BASELINE.json configs[1]): InterNet int_5_len_3, 256x512, bf16 compute, per-GPU
+batch 8 synthetic Cityscapes-shaped triplets resident in HBM; one step = the reference's
+InterTrainer step body (HRNet fwd, RGBLoss (L1+GDL+SSIM+VGG19) + 30*CE, backward, RCCL
+gradient all-reduce, Adamax).  Metric: synthesized frames/s (one per clip), whole job.
+
+After the timed region, 2 extra profiling steps time every plan op with HIP events on the
+launch stream; the dominant kernel family (conv_igemm: forward + data-gradient implicit
+GEMM) is reported against the bf16 MFMA peak as `roofline`.  Rank 0 at N=1 also times the
+CPU oracle (the reference algorithm restated in PyTorch-CPU fp32) on a bounded sample as
+`cpu_baseline`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0  # dense MFMA (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (clips)")
+    ap.add_argument("--height", type=int, default=256)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def make_batch(n, H, W, device, first):
+    from deep_video_interpolation_extrapolation_amd.data import SyntheticClips
+    ds = SyntheticClips(first + n, H, W, 3)
+    items = [ds[first + i] for i in range(n)]
+    return {k: torch.stack([it[k] for it in items]).to(device) for k in items[0]}
+
+
+def cpu_baseline(H, W):
+    """CPU oracle step (reference algorithm, fp32) on a bounded sample."""
+    from oracle import hrnet, losses, step
+    threads = torch.get_num_threads()
+    P = hrnet.init_params(1024)
+    vs = losses.synthetic_vgg19_state()
+    warm = step.synthetic_batch(1, 64, 128)
+    step.inter_step(P, vs, warm)
+    B = 2
+    data = step.synthetic_batch(B, H, W)
+    t = time.time()
+    step.inter_step(P, vs, data)
+    dt = time.time() - t
+    return {"value": B / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"1 InterTrainer step of the CPU oracle (fp32) at {H}x{W}, batch {B}, after a 64x128 warm-up; "
+                      f"{dt:.1f}s"}
+
+
+def main():
+    a = parse()
+    os.environ["DVIE_PRECISION"] = a.precision
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from deep_video_interpolation_extrapolation_amd import engine
+    from deep_video_interpolation_extrapolation_amd.options import default_args
+    from deep_video_interpolation_extrapolation_amd.runners.InterTrainer import InterTrainer
+
+    args = default_args("INTER", syn_type="inter", mode="xs2xs", interval=5, vid_length=1, train_coarse=True,
+                        batch_size=a.batch * world, input_h=a.height, input_w=a.width, precision=a.precision,
+                        synthetic=a.batch * world, num_workers=0, split="train", rank=rank, gpus=world)
+    torch.manual_seed(args.seed)
+    trainer = InterTrainer(args)
+    data = make_batch(a.batch, a.height, a.width, dev, rank * a.batch)
+
+    for _ in range(a.warmup):
+        trainer.step(data)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ld = trainer.step(data)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    loss_all = float(ld["loss_all"])
+
+    # ---- profiling steps: per-op HIP events on the launch stream ----
+    prof = []
+    if a.profile_steps > 0:
+        engine.PROFILE = prof
+        for _ in range(a.profile_steps):
+            trainer.step(data)
+        torch.cuda.synchronize()
+        engine.PROFILE = None
+    agg = {}
+    for meta, kind, e0, e1 in prof:
+        ms = e0.elapsed_time(e1)
+        cls = meta["cls"] if meta else f"kind{kind}"
+        r = agg.setdefault(cls, dict(ms=0.0, n=0, flops=0.0, bytes=0.0))
+        r["ms"] += ms
+        r["n"] += 1
+        if meta:
+            r["flops"] += meta.get("flops", 0.0)
+            r["bytes"] += meta.get("bytes", 0.0)
+    conv = [agg[c] for c in ("conv_fwd", "conv_dgrad") if c in agg]
+    roof = None
+    if conv:
+        ms = sum(r["ms"] for r in conv)
+        n = sum(r["n"] for r in conv)
+        fl = sum(r["flops"] for r in conv)
+        tf = fl / (ms * 1e-3) / 1e12
+        peak = PEAK_BF16_TFLOPS if a.precision == "bf16" else PEAK_FP32_TFLOPS
+        roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
+                "traffic": None, "kernel": "conv_igemm_kernel (fwd + dgrad launches)",
+                "launches_per_step": n // max(1, a.profile_steps),
+                "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
+                "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4)}
+
+    if rank == 0:
+        frames = a.batch * world * a.steps
+        out = {
+            "metric": "train frames/s (256x512 len-3 clips)",
+            "value": round(frames / dt, 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt * 1e3 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.precision,
+            "data": "synthetic (seeded Cityscapes-shaped triplets, HBM-resident); random-init HRNet, synthetic VGG19",
+            "config": {"workload": f"InterNet int_5_len_3 train step {a.height}x{a.width} {a.precision}",
+                       "per_gpu_batch": a.batch, "global_batch": a.batch * world, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "loss_all": loss_all,
+            "step_breakdown_ms": {k: round(v["ms"] / max(1, a.profile_steps), 3) for k, v in sorted(agg.items())},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a.height, a.width)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

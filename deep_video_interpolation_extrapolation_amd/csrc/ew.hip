@@ -141,7 +141,8 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p) {
           const int ch = c + k;
           if (ch < p.ext_c) {
             float* d = p.ext + (long long)n * p.sn + (long long)ch * p.sc + (long long)y * p.sh + (long long)x * p.sw;
-            *d = p.beta ? *d + a[k] : a[k];
+            const float v = p.std ? a[k] / p.std[ch] : a[k];  // adjoint of preprocess_norm
+            *d = p.beta ? *d + v : v;
           }
         }
         continue;

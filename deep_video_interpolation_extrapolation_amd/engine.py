@@ -26,6 +26,7 @@ import torch
 from . import _lib as L
 
 PADC = 8  # channel padding granule (16-byte bf16 vectors)
+PROFILE = None  # set to a list to time every op with HIP events (bench profiling steps)
 
 
 def rup(x, m):
@@ -456,6 +457,7 @@ class Plan:
                     s = torch.tensor(_IMAGENET_STD + [1.0] * 5, dtype=torch.float32, device=self.device)
                     self.keep += [m, s]
                     o.u.ew.mean, o.u.ew.std = m.data_ptr(), s.data_ptr()
+                    op.std_t = s
                 self.ext_in.setdefault(op.key, []).append((len(self.fwd), op))
                 self.fwd.append(o)
             elif isinstance(op, ConvOp):
@@ -468,6 +470,11 @@ class Plan:
                     res=self.ptr(op.res) if op.res is not None else None,
                     res_ld=op.res.buf.C if op.res is not None else 0, act=op.act,
                     out_f32=(out.buf.dt == torch.float32 and self.dtype != torch.float32))
+                npx = nf * out.H * out.W
+                o.meta = dict(cls="conv_fwd", name=lay.name,
+                              flops=2.0 * npx * lay.cout * lay.cin * lay.kh * lay.kw,
+                              bytes=float(self.es * (nf * x.H * x.W * lay.cin + npx * lay.cout * (2 if op.res is not None else 1)
+                                                     + lay.cout * lay.cin * lay.kh * lay.kw)))
                 if ext:
                     self.ext_out.setdefault(out.buf.name, []).append((len(self.fwd), out))
                 self.fwd.append(o)
@@ -562,6 +569,11 @@ class Plan:
         g = self.g
         nb = self.nb
         self.wg_first = {}
+        self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
+        self._uses_left = {}
+        for op in g.ops:
+            if isinstance(op, ConvOp) and op.layer.trainable:
+                self._uses_left[op.layer] = self._uses_left.get(op.layer, 0) + 1
         for key, (region, ch) in g.outputs.items():
             b = region.buf
             assert b.needs_grad and b.expected == 0 and all(p.act == L.ACT_NONE for p in b.producers)
@@ -597,6 +609,8 @@ class Plan:
                 if op.requires_grad:
                     o = self.ew_desc(L.EW_TONCHW, nb, out.H, out.W, out.c, 0, 0, [(gout, gld, out.H, out.W)])
                     o.u.ew.ext_c = op.ext_c
+                    if op.normalize:
+                        o.u.ew.std = op.std_t.data_ptr()
                     self.ext_grad.setdefault(op.key, []).append((len(self.bwd), op))
                     self.bwd.append(o)
                 continue
@@ -651,6 +665,9 @@ class Plan:
             d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], 1, 1
             d.splits, d.dtype = splits, self.dt
             self.ws_floats = max(self.ws_floats, splits * lay.cout_p * ntap * x.c)
+            o.meta = dict(cls="conv_wgrad", name=lay.name, flops=2.0 * npix * lay.cout * lay.cin * ntap,
+                          bytes=float(self.es * (npix * lay.cout + nb * x.H * x.W * lay.cin)
+                                      + 4 * splits * lay.cout_p * ntap * x.c))
             self.bwd.append(o)
             o = self._op(L.OP_WREDUCE)
             r = o.u.wreduce
@@ -677,6 +694,9 @@ class Plan:
                 self.bwd.append(o)
                 self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
             self.wg_first[lay] = True
+            self._uses_left[lay] -= 1
+            if self._uses_left[lay] == 0:
+                self.completions.append((len(self.bwd), lay))
         if op.res is not None and op.res.buf.needs_grad:
             self._contrib(op.res, None, ident=(gout, gld))
         if x.buf.needs_grad:
@@ -686,10 +706,18 @@ class Plan:
             def em(beta, res, res_ld, dact, z, z_ld, phases=phases, x=x, xg=xg, out=out, gout=gout, gld=gld, lay=lay):
                 ops = []
                 for ph, wt, kpad in phases:
-                    ops.append(self.conv_desc(
+                    o = self.conv_desc(
                         gout, gld, nb, out.H, out.W, lay.cout_p, wt.data_ptr(), kpad, x.c, ph["oh"], ph["ow"], 1, 1,
                         ph, xg, x.buf.C, x.H, x.W, osy=lay.stride, osx=lay.stride, ory=ph["ry"], orx=ph["rx"],
-                        res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta))
+                        res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)
+                    npx = nb * ph["oh"] * ph["ow"]
+                    frac = npx / float(nb * x.H * x.W)
+                    o.meta = dict(cls="conv_dgrad", name=lay.name,
+                                  flops=2.0 * npx * lay.cin * lay.cout * ph["th"] * ph["tw"],
+                                  bytes=float(self.es * (frac * nb * out.H * out.W * lay.cout
+                                                         + npx * lay.cin * (1 + (res is not None) + (z is not None) + beta)
+                                                         + lay.cout * lay.cin * ph["th"] * ph["tw"])))
+                    ops.append(o)
                 return ops
 
             self._contrib(x, em)
@@ -767,16 +795,41 @@ class Plan:
             if first:
                 d.beta = int(accumulate)
 
+    def _run(self, arr, start, end, s, what, metas):
+        lib = L.load()
+        base = ctypes.addressof(arr)
+        sz = ctypes.sizeof(L.Op)
+        if PROFILE is None:
+            L.check(lib.dvie_run_ops(base + start * sz, end - start, s), what)
+            return
+        for i in range(start, end):  # op-by-op with events (profiling steps only)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(lib.dvie_run_ops(base + i * sz, 1, s), what)
+            e1.record()
+            PROFILE.append((metas[i] if metas is not None else None, arr[i].kind, e0, e1))
+
     def run_forward(self, stream=None):
         s = L.stream_ptr() if stream is None else stream
-        L.check(L.load().dvie_run_ops(ctypes.addressof(self.fwd_arr), len(self.fwd_arr), s), "forward plan")
+        metas = [None] + [getattr(o, "meta", None) for o in self.fwd]
+        self._run(self.fwd_arr, 0, len(self.fwd_arr), s, "forward plan", metas)
         self.generation += 1
 
-    def run_backward(self, stream=None):
+    def run_backward(self, stream=None, cuts=(), on_cut=None):
+        """Run the backward list; with `cuts` (op indices), run it in segments and call
+        on_cut(k) after segment k (used to launch gradient all-reduce buckets as soon as
+        their parameters are final, overlapping communication with the rest)."""
         if self.n_bwd == 0:
             return
         s = L.stream_ptr() if stream is None else stream
-        L.check(L.load().dvie_run_ops(ctypes.addressof(self.bwd_arr), self.n_bwd, s), "backward plan")
+        metas = [getattr(o, "meta", None) for o in self.bwd]
+        start = 0
+        for k, end in enumerate(list(cuts) + [self.n_bwd]):
+            if end > start:
+                self._run(self.bwd_arr, start, end, s, "backward plan", metas)
+            start = max(start, end)
+            if on_cut is not None and k < len(cuts):
+                on_cut(k)
 
     def zero_grad_buffers(self):
         for b in self.g.buffers:

@@ -442,14 +442,45 @@ class HRNet(FlatParams, nn.Module):
         plan.run_forward()
         return plan, (rgb.permute(0, 3, 1, 2)[:, :self.rgb_out_dim], segout.permute(0, 3, 1, 2)[:, :self.seg_out_dim])
 
+    # set by runners.comm.GradSync: (bucket_bytes, fn(lo, hi)) called as soon as the flat
+    # gradient range [lo, hi) is final during the backward pass
+    grad_hook = None
+
+    def _buckets(self, plan, bucket_bytes):
+        key = ("buckets", bucket_bytes)
+        if key in plan.__dict__:
+            return plan.__dict__[key]
+        end = {}
+        for p, (off, n, _) in zip(self._flat_params, self._flat_specs):
+            end[id(p)] = off + n
+        total = self._flat.numel()
+        cuts, ranges, last, hi, done = [], [], 0, 0, 0
+        for idx, lay in plan.completions:
+            ps = [lay.m.weight] + ([lay.m.bias] if lay.m.bias is not None else [])
+            hi = max([hi] + [end[id(p)] for p in ps])
+            done += sum(p.numel() for p in ps)
+            assert done == hi, "parameter gradients must complete in flat-buffer order"
+            if (hi - last) * 4 >= bucket_bytes and hi < total:
+                cuts.append(idx)
+                ranges.append((last, hi))
+                last = hi
+        ranges.append((last, total))
+        plan.__dict__[key] = (cuts, ranges)
+        return cuts, ranges
+
     def run_backward(self, plan, inputs, grads, needs):
-        n = inputs[0].shape[0]
         accumulate = self.grad_views()
         plan.set_param_grads(accumulate)
         g_rgb, g_seg = grads
         plan.set_output_grad("rgb", g_rgb.float())
         plan.set_output_grad("segout", g_seg.float())
-        plan.run_backward()
+        hook = self.grad_hook
+        if hook is None:
+            plan.run_backward()
+        else:
+            cuts, ranges = self._buckets(plan, hook[0])
+            plan.run_backward(cuts=cuts, on_cut=lambda k: hook[1](*ranges[k]))
+            hook[1](*ranges[-1])
         return [None, None]
 
     def forward_split(self, x, seg):

@@ -1,0 +1,217 @@
+"""InterTrainer on the MI355X path (reference runners/InterTrainer.py).
+
+Surface kept from the reference (main.py:85-119 drives it unchanged): __init__(args),
+set_epoch, train, validate, save_checkpoint, load_checkpoint; the loop body of the
+reference (l.380-441) is factored into `step(data) -> loss_dict`, the hot path:
+
+  HRNet plan forward (HIP)  ->  RGBLoss: L1 + GDL + SSIM kernels, VGG19 plan (HIP)
+  -> CE kernel  ->  loss_all / W backward (HRNet + VGG backward plans, HIP; gradient
+  buckets all-reduced over RCCL while the backward still runs)  ->  fused Adamax (HIP).
+
+Differences from the reference, all documented: DDP is replaced by runners.comm.GradSync
+(identical gradient scaling, see there); the 6 scalar loss all-reduces are one coalesced
+all-reduce issued after the optimizer step (values only); tensorboard image logging is
+replaced by scalar JSON lines (tensorboardX is not part of this image).
+"""
+import json
+import os
+import time
+from collections import OrderedDict
+
+import torch
+import torch.distributed as dist
+
+from .. import nets
+from ..data import batch_to, get_dataset
+from ..losses import IoU, L1Loss, PSNR, RGBLoss, SegCrossEntropy, SSIM, VGGCosineLoss
+from ..optim import Adamax
+from ..utils.net_utils import AverageMeter
+from . import comm
+
+
+def get_model(args):
+    return nets.__dict__[args.model](args)
+
+
+def count_parameters(model):
+    return sum(p.numel() for p in model.parameters() if p.requires_grad)
+
+
+class _Log:
+    def info(self, msg):
+        print(msg, flush=True)
+
+
+class InterTrainer:
+    def __init__(self, args):
+        self.args = args
+        self.log = getattr(args, "logger", None) or _Log()
+        self.rank = getattr(args, "rank", 0)
+        self.W = comm.world()
+        args.gpus = getattr(args, "gpus", self.W) or self.W
+        local = int(os.environ.get("LOCAL_RANK", self.rank % max(1, torch.cuda.device_count() or 1)))
+        self.device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        self.log.info("Initializing trainer")
+        model = get_model(args)
+        if not getattr(args, "train_coarse", False):
+            for p in model.coarse_model.parameters():
+                p.requires_grad = False
+        self.log.info("coarse params " + str(count_parameters(model.coarse_model)))
+        model.to(self.device)
+        self.model = comm.GradSync(model)
+        self.global_step = 0
+        self.epoch = 1
+        if args.split in ("train", "val"):
+            self.train_set, self.val_set = get_dataset(args)
+        if args.split == "train":
+            self.RGBLoss = RGBLoss(args).to(self.device)
+            self.SegLoss = SegCrossEntropy()
+            self.coarse_opt = Adamax(list(self.model.module.coarse_model.parameters()), lr=args.coarse_learning_rate)
+            sampler = torch.utils.data.distributed.DistributedSampler(self.train_set) if self.W > 1 else None
+            self.train_loader = torch.utils.data.DataLoader(
+                self.train_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
+                num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
+        elif args.split == "val":
+            self.L1Loss, self.PSNRLoss, self.SSIMLoss = L1Loss(), PSNR(), SSIM()
+            self.IoULoss, self.VGGCosLoss = IoU(), VGGCosineLoss().to(self.device)
+            sampler = torch.utils.data.distributed.DistributedSampler(self.val_set) if self.W > 1 else None
+            self.val_loader = torch.utils.data.DataLoader(
+                self.val_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
+                num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
+        if getattr(args, "resume", False) or getattr(args, "load_coarse", False):
+            self.load_checkpoint()
+
+    # ---------------- the hot path ----------------
+    def get_input(self, data):
+        gt_x = data["frame2"]
+        gt_seg = data["seg2"] if self.args.mode == "xs2xs" else None
+        x = torch.cat([data["frame1"], data["frame3"]], dim=1)
+        seg = torch.cat([data["seg1"], data["seg3"]], dim=1) if self.args.mode == "xs2xs" else None
+        return x, seg, gt_x, gt_seg
+
+    def step(self, data):
+        """One training step (reference l.389-437).  data: sample dict (any device)."""
+        data = batch_to(data, self.device)
+        x, seg, gt_x, gt_seg = self.get_input(data)
+        loss_dict = OrderedDict()
+        coarse_img, coarse_seg = self.model(x, seg=seg)
+        prefix = "coarse"
+        loss_dict.update(self.RGBLoss(coarse_img, gt_x, False, prefix=prefix))
+        if self.args.mode == "xs2xs":
+            loss_dict[prefix + "_ce_loss"] = self.args.ce_weight * self.SegLoss(coarse_seg, gt_seg)
+        loss = 0
+        for v in loss_dict.values():
+            loss = loss + torch.mean(v)
+        loss_dict["loss_all"] = loss
+        self.coarse_opt.zero_grad(set_to_none=True)
+        # reference `sync` divides loss_all by W in place before backward (l.431, 859-864)
+        (loss / self.W).backward()
+        self.model.finish()
+        if getattr(self.args, "train_coarse", False):
+            self.coarse_opt.step()
+        self.global_step += 1
+        return comm.sync_losses(OrderedDict((k, v.detach()) for k, v in loss_dict.items()), self.W)
+
+    # ---------------- loops ----------------
+    def set_epoch(self, epoch):
+        self.log.info("Start of epoch %d" % (epoch + 1))
+        self.epoch = epoch + 1
+        if isinstance(getattr(self.train_loader, "sampler", None), torch.utils.data.distributed.DistributedSampler):
+            self.train_loader.sampler.set_epoch(epoch)
+
+    def train(self):
+        if self.rank == 0:
+            self.log.info("Training started")
+        self.model.train()
+        meters = OrderedDict()
+        end = time.time()
+        load_time = comp_time = 0.0
+        for step, data in enumerate(self.train_loader):
+            self.step_idx = step
+            load_time += time.time() - end
+            end = time.time()
+            loss_dict = self.step(data)
+            comp_time += time.time() - end
+            end = time.time()
+            if self.rank == 0:
+                bs = data["frame1"].size(0)
+                for k, v in loss_dict.items():
+                    meters.setdefault(k, AverageMeter()).update(float(v), bs)
+                if step % self.args.disp_interval == 0:
+                    msg = "Epoch [{}/{}][{}/{}] load [{:.3f}s] comp [{:.3f}s] ".format(
+                        self.epoch, self.args.epochs, step + 1, len(self.train_loader), load_time, comp_time)
+                    msg += " ".join(f"{k} [{m.avg:.3f}]" for k, m in meters.items())
+                    self.log.info(msg)
+                    self._scalars("losses", {k: m.avg for k, m in meters.items()})
+                    meters = OrderedDict()
+                    load_time = comp_time = 0.0
+
+    def normalize(self, img):
+        return (img + 1) / 2
+
+    def validate(self):
+        self.log.info("Validation epoch {} started".format(self.epoch))
+        self.model.eval()
+        crit = ["coarse_l1", "coarse_psnr", "coarse_ssim", "coarse_vgg"] + (["coarse_iou"] if self.args.mode == "xs2xs" else [])
+        meters = {c: AverageMeter() for c in crit}
+        with torch.no_grad():
+            for i, data in enumerate(self.val_loader):
+                data = batch_to(data, self.device)
+                x, seg, gt_x, gt_seg = self.get_input(data)
+                coarse_img, coarse_seg = self.model(x, seg=seg)
+                coarse_img = coarse_img.clamp(-1, 1)
+                a, b = self.normalize(coarse_img), self.normalize(gt_x)
+                d = OrderedDict()
+                d["coarse_l1"] = self.L1Loss(a, b)
+                d["coarse_psnr"] = self.PSNRLoss(a, b)
+                d["coarse_ssim"] = 1 - self.SSIMLoss(a, b)
+                if self.args.mode == "xs2xs":
+                    d["coarse_iou"] = self.IoULoss(torch.argmax(coarse_seg, dim=1), torch.argmax(gt_seg, dim=1))
+                d["coarse_vgg"] = self.VGGCosLoss(a, b, False)
+                d = comm.sync_losses(d, self.W)
+                if self.rank == 0:
+                    for c in crit:
+                        meters[c].update(float(d[c]), data["frame1"].size(0) * self.W)
+        res = {c: m.avg for c, m in meters.items()}
+        if self.rank == 0:
+            self.log.info("Epoch [{}] Evaluation: ".format(self.epoch) + " ".join(f"{k} [{v:.3f}]" for k, v in res.items()))
+            self._scalars("val/score", res)
+        return res
+
+    def _scalars(self, tag, info):
+        path = getattr(self.args, "path", None)
+        if path:
+            with open(os.path.join(path, "scalars.jsonl"), "a") as f:
+                f.write(json.dumps(dict(tag=tag, step=self.global_step, **info)) + "\n")
+
+    # ---------------- checkpoints (reference l.867-960) ----------------
+    def _ckpt_name(self, model_name, session, epoch, step, root):
+        d = "{}_{}_{}_{}".format(model_name, self.args.mode, self.args.syn_type, session)
+        return os.path.join(root, "checkpoint", d + "_{}_{}.pth".format(epoch, step))
+
+    def save_checkpoint(self):
+        name = self._ckpt_name(self.args.model, self.args.session, self.epoch, getattr(self, "step_idx", 0),
+                               self.args.path)
+        os.makedirs(os.path.dirname(name), exist_ok=True)
+        torch.save({"session": self.args.session, "epoch": self.epoch + 1,
+                    "coarse_model": self.model.module.coarse_model.state_dict(),
+                    "coarse_opt": self.coarse_opt.state_dict()}, name)
+        self.log.info("save model: {}".format(name))
+        return name
+
+    def load_checkpoint(self):
+        a = self.args
+        name = self._ckpt_name(a.load_model, a.checksession, a.checkepoch, a.checkpoint, a.load_dir or ".")
+        self.log.info("Loading checkpoint %s" % name)
+        ckpt = torch.load(name, map_location="cpu", weights_only=True)
+        if getattr(a, "load_coarse", False) or getattr(a, "resume", False):
+            sd = self.model.module.coarse_model.state_dict()
+            sd.update(ckpt["coarse_model"])
+            self.model.module.coarse_model.load_state_dict(sd)
+        if a.split == "train" and getattr(a, "train_coarse", False) and "coarse_opt" in ckpt:
+            self.coarse_opt.load_state_dict(ckpt["coarse_opt"])
+        if getattr(a, "resume", False):
+            self.epoch = ckpt["epoch"]
+        self.log.info("checkpoint loaded")

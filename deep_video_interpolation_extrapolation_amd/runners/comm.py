@@ -1,0 +1,87 @@
+"""Data-parallel gradient synchronisation over RCCL (torch.distributed 'nccl' on ROCm).
+
+Replaces DistributedDataParallel (runners/InterTrainer.py:63-64) for plan-executed models:
+parameters live in one flat fp32 buffer laid out in backward-completion order, so the
+gradient all-reduce is a handful of large contiguous buckets launched from inside the
+backward pass as soon as each bucket's weight reductions are enqueued (RCCL runs on its
+own stream, overlapping the remaining backward kernels).  The loss-value sync of the
+reference (`sync`, l.859-864: one all_reduce per scalar) is one coalesced all_reduce.
+
+Gradient scaling follows the reference exactly: each rank back-propagates loss_all / W
+(the in-place div_ of `sync` is recorded by autograd) and DDP averages, so the applied
+gradient is (1/W) * mean_r grad(L_r); here: SUM all-reduce, then x 1/W.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+from .. import _lib as L
+
+
+def world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank():
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+class GradSync:
+    """`self.model = GradSync(model)` keeps `self.model.module` like DDP does."""
+
+    def __init__(self, module, bucket_mb=None):
+        self.module = module
+        self.W = world()
+        self.bucket_bytes = int(float(bucket_mb or os.environ.get("DVIE_BUCKET_MB", 16)) * 2 ** 20)
+        self.flat_owners = [m for m in module.modules() if hasattr(m, "_flat")]
+        self.works = []
+        if self.W > 1:
+            for m in self.flat_owners:  # DDP's initial parameter broadcast
+                dist.broadcast(m._flat, 0)
+                m.grad_hook = (self.bucket_bytes, self._make_hook(m))
+
+    def _make_hook(self, owner):
+        def hook(lo, hi):
+            if hi > lo:
+                self.works.append(dist.all_reduce(owner._flat_grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+        return hook
+
+    def __call__(self, *a, **k):
+        return self.module(*a, **k)
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["module"], name)
+
+    def finish(self):
+        """Wait for the bucket all-reduces (stream-ordered) and apply the 1/W factor."""
+        if self.W == 1:
+            return
+        for w in self.works:
+            w.wait()
+        self.works = []
+        lib = L.load()
+        for m in self.flat_owners:
+            g = m._flat_grad
+            if g is not None:
+                L.check(lib.dvie_scale(g.data_ptr(), g.numel(), 1.0 / self.W, L.stream_ptr(g.device)), "grad scale")
+
+    def train(self, mode=True):
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+
+def sync_losses(loss_dict, W):
+    """Mean over ranks of every logged scalar, as one all_reduce (values only)."""
+    if W == 1:
+        return loss_dict
+    keys = list(loss_dict.keys())
+    flat = torch.stack([loss_dict[k].detach().float().reshape(()) for k in keys])
+    dist.all_reduce(flat)
+    flat /= W
+    for i, k in enumerate(keys):
+        loss_dict[k] = flat[i]
+    return loss_dict

@@ -50,6 +50,8 @@ class FlatParams:
             flat[off:off + n].copy_(p.detach().reshape(-1))
             specs.append((off, n, tuple(p.shape)))
             off += n
+        for p in params:
+            p._dvie_owner = self  # lets optim.Adamax take the one-launch flat path
         self._flat_params = params
         self._flat_specs = specs
         self._flat = flat

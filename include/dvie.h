@@ -165,8 +165,9 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
  *  DVIE_EW_NCHW   y = ext (fp32, arbitrary NCHW strides sn,sc,sh,sw; channels >= ext_c
  *                 read as zero), optionally (ext - mean[c]) / std[c]
  *                 (preprocess_norm, utils/net_utils.py:11-23).
- *  DVIE_EW_TONCHW ext (+)= channels [0, ext_c) of src_0 as fp32 with NCHW strides
- *                 (beta selects accumulate; the NHWC epilogue is not applied).
+ *  DVIE_EW_TONCHW ext (+)= channels [0, ext_c) of src_0 as fp32 with NCHW strides,
+ *                 divided by std[c] when std is set (adjoint of the normalisation);
+ *                 beta selects accumulate; the NHWC epilogue is not applied.
  * then the shared epilogue: v += res; v += y_old (beta); v = act(v); v *= act'(z); y = v.
  * Channels c % 4 == 0; all lds % 4 == 0.
  */

@@ -88,7 +88,7 @@ def _lrelu(x):
     return F.leaky_relu(x, 0.2)
 
 
-def forward(P, inp, n_frames=2, large=False):
+def forward(P, inp, n_frames=2, large=False, taps=None):
     """HRNet.forward (nets/HRNet.py:524-601) for syn_type 'inter' (and 'extra' without
     inpainting).  inp: (B, 3F + 20F, H, W).  Returns (rgb, seg_logits)."""
     F_ = n_frames
@@ -131,8 +131,12 @@ def forward(P, inp, n_frames=2, large=False):
             h = x_list[i]
             for b in range(4):
                 o = _lrelu(_conv(P, f"{st}.branches.{i}.{b}.conv1", h))
+                if taps is not None:
+                    taps[f"{st}.branches.{i}.{b}.h"] = o
                 o = _conv(P, f"{st}.branches.{i}.{b}.conv2", o)
                 h = _lrelu(o + h)
+                if taps is not None:
+                    taps[f"{st}.branches.{i}.{b}.out"] = h
             xs.append(h)
         ys = []
         for i in range(nb):  # HighResolutionModule.forward fuse (l.211-225)

@@ -153,23 +153,34 @@ def test_hrnet_forward_fp32_parity(dev, monkeypatch):
 
 
 def test_hrnet_backward_fp32_parity(dev, monkeypatch):
+    """Parameter gradients vs an fp64 oracle's autograd.
+
+    Metric: per-tensor relative L2 error.  A max-abs metric is ill-conditioned here: an
+    activation that fp64 puts at +1e-9 and fp32 at -1e-9 flips LeakyReLU's derivative
+    (1 vs 0.2) at that pixel, which moves single gradient entries by O(1) relative
+    (observed: 1 such flip in ~5e6 activations, |a| = 7.9e-9).  Tolerances: every
+    tensor < 2e-2 relative L2, median tensor < 1e-5 (fp32 rounding level)."""
     m = _hrnet(dev, "fp32", monkeypatch)
-    P = {k: v.clone().requires_grad_(True) for k, v in O.init_params(1024).items()}
+    P0 = O.init_params(1024)
     x, seg = inputs.hrnet_input(2, 32, 64)
     g = torch.Generator().manual_seed(5)
     w1 = torch.randn((2, 3, 32, 64), generator=g)
     w2 = torch.randn((2, 20, 32, 64), generator=g)
     rgb, s = m(x.to(dev), seg.to(dev))
     ((rgb * w1.to(dev)).sum() + (s * w2.to(dev)).sum()).backward()
-    rr, sr = O.forward(P, torch.cat([x, seg], 1))
-    ((rr * w1).sum() + (sr * w2).sum()).backward()
+    P = {k: v.double().clone().requires_grad_(True) for k, v in P0.items()}
+    rr, sr = O.forward(P, torch.cat([x, seg], 1).double())
+    ((rr * w1.double()).sum() + (sr * w2.double()).sum()).backward()
     named = dict(m.coarse_model.named_parameters())
-    worst = 0.0
-    for k, p in P.items():
-        e = rel_err(named[k].grad, p.grad)
-        worst = max(worst, e)
-        assert e < 2e-3, (k, e)
-    print("worst relative grad error", worst)
+    errs = {}
+    for k in P0:
+        a, b = named[k].grad.detach().cpu().double(), P[k].grad
+        errs[k] = float((a - b).norm() / b.norm())
+    worst = max(errs, key=errs.get)
+    med = float(np.median(list(errs.values())))
+    print(f"grad rel-L2: median {med:.2e}, worst {errs[worst]:.2e} ({worst})")
+    assert errs[worst] < 2e-2, (worst, errs[worst])
+    assert med < 1e-5, med
 
 
 def test_hrnet_bf16_close_to_fp32(dev, monkeypatch):
