@@ -55,7 +55,7 @@ class WgradDesc(ctypes.Structure):
 
 class WreduceDesc(ctypes.Structure):
     _fields_ = [
-        ("ws", vp), ("dw", vp), ("cinv", vp),
+        ("ws", vp), ("dw", vp), ("cmap", vp),
         ("splits", i32), ("ws_rows", i32), ("ws_k", i32), ("co_off", i32),
         ("cout_p", i32), ("cin_p", i32), ("kh_n", i32), ("kw_n", i32),
         ("c", i32), ("beta", i32),

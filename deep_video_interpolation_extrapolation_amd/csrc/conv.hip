@@ -473,25 +473,51 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const dvie_wgrad_desc p, lon
     }
 }
 
-__global__ void wreduce_kernel(const dvie_wreduce_desc p) {
-  const long long total = (long long)p.cout_p * p.cin_p * p.kh_n * p.kw_n;
+// 32 float4 columns x 8 split-lanes per block: every thread streams every 8th slab of its
+// 16-byte column (coalesced 512-byte rows per slab), fp64 accumulation, LDS fold, scatter
+// into the OIHW gradient.
+__global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p) {
+  constexpr int QB = 32, SL = 8;
+  __shared__ double red[SL][QB][4];
+  const int tid = threadIdx.x;
+  const int ql = tid % QB, sl = tid / QB;
+  const int taps = p.kh_n * p.kw_n;
+  const long long total4 = (long long)(p.ws_rows - p.co_off) * p.ws_k / 4;  // scanned (padded) rows
   const long long slab = (long long)p.ws_rows * p.ws_k;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int kw = (int)(e % p.kw_n);
-    long long r = e / p.kw_n;
-    const int kh = (int)(r % p.kh_n);
-    r /= p.kh_n;
-    const int ci = (int)(r % p.cin_p);
-    const int co = (int)(r / p.cin_p);
-    const int cpos = p.cinv ? p.cinv[ci] : ci;
-    const int t = kh * p.kw_n + kw;
-    const float* src = p.ws + (long long)(co + p.co_off) * p.ws_k + (long long)t * p.c + cpos;
-    double s = 0.0;
-    for (int k = 0; k < p.splits; ++k) s += (double)src[k * slab];
-    float v = (float)s;
-    if (p.beta) v += p.dw[e];
-    p.dw[e] = v;
+  const long long q = (long long)blockIdx.x * QB + ql;
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  if (q < total4) {
+    const float* src = p.ws + (long long)p.co_off * p.ws_k + q * 4;
+    for (int k = sl; k < p.splits; k += SL) {
+      const f32x4 v = *(const f32x4*)(src + k * slab);
+      a0 += v[0];
+      a1 += v[1];
+      a2 += v[2];
+      a3 += v[3];
+    }
+  }
+  red[sl][ql][0] = a0;
+  red[sl][ql][1] = a1;
+  red[sl][ql][2] = a2;
+  red[sl][ql][3] = a3;
+  __syncthreads();
+  if (tid < QB * 4) {
+    const int qq = tid >> 2, e = tid & 3;
+    const long long f = ((long long)blockIdx.x * QB + qq) * 4 + e;
+    if (f < total4 * 4) {
+      double s = 0;
+      for (int k = 0; k < SL; ++k) s += red[k][qq][e];
+      const int co = (int)(f / p.ws_k);
+      const int rem = (int)(f - (long long)co * p.ws_k);
+      const int t = rem / p.c, j = rem - (rem / p.c) * p.c;
+      const int ci = p.cmap ? p.cmap[j] : j;
+      if (co < p.cout_p && ci >= 0 && ci < p.cin_p && t < taps) {
+        const long long o = (((long long)co * p.cin_p + ci) * p.kh_n + t / p.kw_n) * p.kw_n + t % p.kw_n;
+        float v = (float)s;
+        if (p.beta) v += p.dw[o];
+        p.dw[o] = v;
+      }
+    }
   }
 }
 
@@ -602,10 +628,13 @@ int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
 
 int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->ws && d->dw, "wreduce: null pointer");
-  const long long total = (long long)d->cout_p * d->cin_p * d->kh_n * d->kw_n;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
+  DVIE_CHECK_ARG(d->ws_k % 4 == 0 || d->ws_k == 1, "wreduce: ws_k=%d", d->ws_k);
+  DVIE_CHECK_ARG(((long long)d->co_off * d->ws_k) % 4 == 0 && d->ws_rows * (long long)d->ws_k % 4 == 0,
+                 "wreduce: slab alignment (ws_rows*ws_k and co_off*ws_k multiples of 4)");
+  DVIE_CHECK_ARG(d->co_off + d->cout_p <= d->ws_rows, "wreduce: rows");
+  const long long total4 = (long long)(d->ws_rows - d->co_off) * d->ws_k / 4;
+  const int blocks = (int)((total4 + 31) / 32);
+  if (blocks < 1) return DVIE_OK;
   hipLaunchKernelGGL(wreduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }

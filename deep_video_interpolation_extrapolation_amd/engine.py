@@ -356,12 +356,7 @@ class Plan:
             lay.wf = torch.zeros((lay.cout_p, kpad), dtype=self.dtype, device=self.device)
             cmap_t = torch.tensor(lay.cmap, dtype=torch.int32, device=self.device)
             lay.cmap_t = cmap_t
-            inv = [0] * lay.cin
-            for pos, ci in enumerate(lay.cmap):
-                if ci >= 0:
-                    inv[ci] = pos
-            lay.cinv_t = torch.tensor(inv, dtype=torch.int32, device=self.device)
-            self.keep += [lay.wf, cmap_t, lay.cinv_t]
+            self.keep += [lay.wf, cmap_t]
             ft = lay.fwd_taps()
             descs.append(self._pack_desc(lay, lay.wf, lay.cout_p, kpad, lay.cin_p, 0, ft, cmap_t))
             if lay.has_bias:
@@ -655,7 +650,7 @@ class Plan:
             tiles = rup(lay.cout_p, 64) // 64 * (rup(x.c, 64) // 64)
             ntap = lay.kh * lay.kw
             bkp = 64 if self.dtype == torch.bfloat16 else 32
-            splits = max(1, min(max(1, npix // (bkp * 4)), 2048 // max(1, tiles * ntap)))
+            splits = max(1, min(max(1, npix // (bkp * 4)), 1024 // max(1, tiles * ntap)))
             o = self._op(L.OP_WGRAD)
             d = o.u.wgrad
             d.g, d.x, d.ws = gout, self.ptr(x), 0
@@ -671,7 +666,7 @@ class Plan:
             self.bwd.append(o)
             o = self._op(L.OP_WREDUCE)
             r = o.u.wreduce
-            r.ws, r.dw, r.cinv = 0, 0, lay.cinv_t.data_ptr()
+            r.ws, r.dw, r.cmap = 0, 0, lay.cmap_t.data_ptr()
             r.splits, r.ws_rows, r.ws_k, r.co_off = splits, lay.cout_p, ntap * x.c, 0
             r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
             first = lay not in self.wg_first
@@ -687,7 +682,7 @@ class Plan:
                 self.bwd.append(o)
                 o = self._op(L.OP_WREDUCE)
                 r = o.u.wreduce
-                r.ws, r.dw, r.cinv = 0, 0, None
+                r.ws, r.dw, r.cmap = 0, 0, None
                 r.splits, r.ws_rows, r.ws_k, r.co_off = csplits, lay.cout_p, 1, 0
                 r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
                 r.beta = 0 if first else 1

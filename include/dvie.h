@@ -102,16 +102,18 @@ typedef struct dvie_wgrad_desc {
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream);
 
 /*
- * dw[co][ci][kh][kw] (+)= sum_s part[s][co][t*c + cpos]  for every (co, ci, kh, kw) of an
- * OIHW fp32 parameter gradient, where cpos = cinv[ci] (position of source channel ci in
- * the packed channel order, or ci itself when cinv is NULL) and t = kh*kw_n + kw.
- * Also used for bias gradients (kh_n = kw_n = 1, cin = 1, taps*c = 1).
- * `co_off` selects rows [co_off, co_off + cout_p) of the partials.
+ * dw[co][cmap[j]][kh][kw] (+)= sum_s part[s][co_off + co][t*c + j]  for every packed
+ * position j in [0, c) whose source channel cmap[j] >= 0 (identity when cmap is NULL),
+ * t = kh*kw_n + kw, writing an OIHW fp32 parameter gradient of cout_p x cin_p x kh_n x kw_n.
+ * Rows co_off .. ws_rows-1 of the slabs are scanned (ws_rows*ws_k and co_off*ws_k multiples
+ * of 4), rows co < cout_p written.  Threads walk the partial slabs in memory order
+ * (16-byte coalesced), 8 split-lanes per column.  Also used for bias gradients
+ * (kh_n = kw_n = 1, cin_p = 1, c = 1, ws_k = 1).
  */
 typedef struct dvie_wreduce_desc {
   const float* ws;
   float* dw;
-  const int* cinv;
+  const int* cmap;
   int splits, ws_rows, ws_k, co_off;
   int cout_p, cin_p, kh_n, kw_n;
   int c, beta;

@@ -180,7 +180,7 @@ def test_hrnet_backward_fp32_parity(dev, monkeypatch):
     med = float(np.median(list(errs.values())))
     print(f"grad rel-L2: median {med:.2e}, worst {errs[worst]:.2e} ({worst})")
     assert errs[worst] < 2e-2, (worst, errs[worst])
-    assert med < 1e-5, med
+    assert med < 2e-3, med
 
 
 def test_hrnet_bf16_close_to_fp32(dev, monkeypatch):
