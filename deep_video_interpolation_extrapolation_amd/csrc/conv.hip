@@ -1,15 +1,6 @@
 // Convolution kernels for gfx950 (MI355X, CDNA4).
 //
-// conv_igemm: NHWC implicit GEMM on MFMA.  rows = output channels (the MFMA "A"
-//   operand, packed weights [cout][kpad]), columns = output pixels (the MFMA "B"
-//   operand, gathered from the NHWC input on the fly, one tap at a time).  Both operands
-//   are K-contiguous in memory, so every global load is a 16-byte vector and both LDS
-//   images use the same 128-byte rows (8 x 16 B chunks, XOR-swizzled by row).
-//   fp32 mode: v_mfma_f32_16x16x4_f32 (exact fp32 fma chain, parity mode);
-//   bf16 mode: v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
-//   Register-staged double buffer: the next K-step's global loads are issued before
-//   the MFMAs of the current one and written to the other LDS buffer after them (one
-//   barrier per K-step).
+// (the implicit-GEMM forward / data-gradient kernel lives in conv_fwd.hip)
 //
 // wgrad: per tap, dW[co][ci] = sum_pix g[pix][co] * x[pix+tap][ci], split over pixel
 //   chunks into fp32 partial slabs (no atomics, deterministic), reduced by wreduce into
@@ -34,231 +25,6 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 const char* last_error() { return g_err; }
-
-// ----------------------------------------------------------------------------------
-// implicit GEMM forward / data-gradient
-// ----------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void mfma_chunk(f32x4& acc, const i32x4& a, const i32x4& b);
-
-template <>
-__device__ __forceinline__ void mfma_chunk<float>(f32x4& acc, const i32x4& a, const i32x4& b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[0]), __int_as_float(b[0]), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[1]), __int_as_float(b[1]), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[2]), __int_as_float(b[2]), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__int_as_float(a[3]), __int_as_float(b[3]), acc, 0, 0, 0);
-}
-
-template <>
-__device__ __forceinline__ void mfma_chunk<bf16_t>(f32x4& acc, const i32x4& a, const i32x4& b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                acc, 0, 0, 0);
-}
-
-// byte offset of 16-byte chunk `ch` (0..7) of LDS row `row` (128-byte rows)
-__device__ __forceinline__ int swz128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
-
-template <typename T, int BC, int BP, int WC, int WP, bool OUTF32>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(const dvie_conv_desc p) {
-  typedef typename std::conditional<OUTF32, float, T>::type OutT;
-  constexpr int ES = sizeof(T);
-  constexpr int VEC = 16 / ES;
-  constexpr int KSTEP = 128 / ES;
-  constexpr int TM = BC / WC / 16;
-  constexpr int TN = BP / WP / 16;
-  constexpr int A_IT = BC / 32;
-  constexpr int B_IT = BP / 32;
-  static_assert(WC * WP == 4, "4 waves");
-  static_assert(BC % 32 == 0 && BP % 32 == 0, "tiles of 32");
-  __shared__ __attribute__((aligned(16))) char smem[2 * (BC + BP) * 128];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wc = wave / WP, wp = wave % WP;
-  const int hw = p.oh * p.ow;
-  const long long npix = (long long)p.n * hw;
-  const long long p0 = (long long)blockIdx.x * BP;
-  const int c0 = blockIdx.y * BC;
-  const int vec = tid & 7;
-  const int ntap = p.th * p.tw;
-  const int K = ntap * p.c;
-  const int CV = p.c / VEC;
-  const int nk = (K + KSTEP - 1) / KSTEP;
-  const char* __restrict__ xg = (const char*)p.x;
-  const char* __restrict__ wg = (const char*)p.w;
-
-  // staged pixel rows of this thread
-  int bn[B_IT], by[B_IT], bx[B_IT];
-#pragma unroll
-  for (int i = 0; i < B_IT; ++i) {
-    const int row = (tid >> 3) + 32 * i;
-    const long long pix = p0 + row;
-    if (pix < npix) {
-      const int n = (int)(pix / hw);
-      const int r = (int)(pix - (long long)n * hw);
-      const int oy = r / p.ow;
-      const int ox = r - oy * p.ow;
-      bn[i] = n;
-      by[i] = oy * p.sy;
-      bx[i] = ox * p.sx;
-    } else {
-      bn[i] = 0;
-      by[i] = -(1 << 28);
-      bx[i] = 0;
-    }
-  }
-  int tap = vec / CV, cv = vec - (vec / CV) * CV;
-
-  i32x4 ra[A_IT], rb[B_IT];
-  auto load_stage = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < A_IT; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      const int co = c0 + row;
-      if (co < p.cout)
-        ra[i] = *(const i32x4*)(wg + ((long long)co * p.kpad + (long long)kt * KSTEP + vec * VEC) * ES);
-      else
-        ra[i] = i32x4{0, 0, 0, 0};
-    }
-    const bool tv = tap < ntap;
-    const int ti = tv ? tap / p.tw : 0;
-    const int tj = tap - ti * p.tw;
-    const int dy = p.dy0 + ti * p.ddy, dx = p.dx0 + tj * p.ddx;
-#pragma unroll
-    for (int i = 0; i < B_IT; ++i) {
-      const int iy = by[i] + dy, ix = bx[i] + dx;
-      if (tv && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw) {
-        const long long off = ((((long long)bn[i] * p.ih + iy) * p.iw + ix) * p.x_ld + (long long)cv * VEC) * ES;
-        rb[i] = *(const i32x4*)(xg + off);
-      } else {
-        rb[i] = i32x4{0, 0, 0, 0};
-      }
-    }
-    cv += 8;
-    while (cv >= CV) {
-      cv -= CV;
-      ++tap;
-    }
-  };
-  auto store_stage = [&](int buf) {
-    char* As = smem + buf * (BC + BP) * 128;
-    char* Bs = As + BC * 128;
-#pragma unroll
-    for (int i = 0; i < A_IT; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *(i32x4*)(As + swz128(row, vec)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_IT; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *(i32x4*)(Bs + swz128(row, vec)) = rb[i];
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
-
-  const int r16 = lane & 15;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_stage(kt + 1);
-    const char* As = smem + cur * (BC + BP) * 128;
-    const char* Bs = As + BC * 128;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = 4 * s + (lane >> 4);
-      i32x4 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wc * (BC / WC) + 16 * i + r16;
-        af[i] = *(const i32x4*)(As + swz128(row, ch));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wp * (BP / WP) + 16 * j + r16;
-        bf[j] = *(const i32x4*)(Bs + swz128(row, ch));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mfma_chunk<T>(acc[i][j], af[i], bf[j]);
-    }
-    if (kt + 1 < nk) store_stage(cur ^ 1);
-    __syncthreads();
-  }
-
-  // epilogue: lane holds 4 consecutive output channels of one pixel per tile
-  OutT* __restrict__ yg = (OutT*)p.y;
-  const OutT* __restrict__ rg = (const OutT*)p.res;
-  const T* __restrict__ zg = (const T*)p.z;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const long long pix = p0 + wp * (BP / WP) + 16 * j + r16;
-    if (pix >= npix) continue;
-    const int n = (int)(pix / hw);
-    const int r = (int)(pix - (long long)n * hw);
-    const int oy = r / p.ow;
-    const int ox = r - oy * p.ow;
-    const long long yrow = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int co = c0 + wc * (BC / WC) + 16 * i + 4 * (lane >> 4);
-      if (co >= p.cout) continue;
-      f32x4 v = acc[i][j];
-      if (p.bias) {
-        v[0] += p.bias[co];
-        v[1] += p.bias[co + 1];
-        v[2] += p.bias[co + 2];
-        v[3] += p.bias[co + 3];
-      }
-      if (rg) v += V4<OutT>::load(rg + yrow * p.res_ld + co);
-      if (p.beta) v += V4<OutT>::load(yg + yrow * p.y_ld + co);
-      if (p.act) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act, p.alpha);
-      }
-      if (p.dact) {
-        const f32x4 z = V4<T>::load(zg + yrow * p.z_ld + co);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] *= act_dz(z[e], p.dact, p.alpha);
-      }
-      V4<OutT>::store(yg + yrow * p.y_ld + co, v);
-    }
-  }
-}
-
-template <typename T, int BC, int BP, int WC, int WP>
-static void launch_conv(const dvie_conv_desc& p, hipStream_t s) {
-  const long long npix = (long long)p.n * p.oh * p.ow;
-  dim3 grid((unsigned)((npix + BP - 1) / BP), (unsigned)((p.cout + BC - 1) / BC));
-  if (p.out_f32)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, BC, BP, WC, WP, true>), grid, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<T, BC, BP, WC, WP, false>), grid, dim3(256), 0, s, p);
-}
-
-template <typename T>
-static void dispatch_conv(const dvie_conv_desc& p, hipStream_t s) {
-  const long long npix = (long long)p.n * p.oh * p.ow;
-  const bool small = npix < 64LL * 512;  // not enough 128-pixel tiles to fill 256 CUs
-  if (p.cout <= 32) {
-    if (small) launch_conv<T, 32, 64, 2, 2>(p, s);
-    else launch_conv<T, 32, 128, 2, 2>(p, s);
-  } else if (p.cout <= 64) {
-    if (small) launch_conv<T, 64, 64, 2, 2>(p, s);
-    else launch_conv<T, 64, 128, 2, 2>(p, s);
-  } else {
-    if (small) launch_conv<T, 128, 64, 2, 2>(p, s);
-    else launch_conv<T, 128, 128, 2, 2>(p, s);
-  }
-}
 
 // ----------------------------------------------------------------------------------
 // weight gradient
@@ -585,27 +351,6 @@ __global__ void pack_kernel(const dvie_pack_desc* __restrict__ descs) {
 using namespace dvie;
 
 extern "C" {
-
-int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
-  DVIE_CHECK_ARG(d && d->x && d->w && d->y, "conv: null pointer");
-  const int vec = d->dtype == DVIE_BF16 ? 8 : 4;
-  DVIE_CHECK_ARG(d->c > 0 && d->c % vec == 0, "conv: c=%d must be a multiple of %d", d->c, vec);
-  DVIE_CHECK_ARG(d->cout > 0 && d->cout % 4 == 0, "conv: cout=%d must be a multiple of 4", d->cout);
-  DVIE_CHECK_ARG(d->kpad % 64 == 0 && d->kpad >= d->th * d->tw * d->c, "conv: kpad=%d", d->kpad);
-  DVIE_CHECK_ARG(d->x_ld % vec == 0 && d->y_ld % 4 == 0, "conv: ld alignment x_ld=%lld y_ld=%lld",
-                 d->x_ld, d->y_ld);
-  DVIE_CHECK_ARG(d->th >= 1 && d->tw >= 1 && d->th * d->tw <= 64, "conv: taps");
-  DVIE_CHECK_ARG(d->n > 0 && d->oh > 0 && d->ow > 0 && d->ih > 0 && d->iw > 0, "conv: empty shape");
-  DVIE_CHECK_ARG(((uintptr_t)d->x & 15) == 0 && ((uintptr_t)d->w & 15) == 0, "conv: x/w not 16B aligned");
-  hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == DVIE_BF16)
-    dispatch_conv<bf16_t>(*d, s);
-  else {
-    DVIE_CHECK_ARG(d->out_f32 || d->dtype == DVIE_F32, "conv: dtype");
-    dispatch_conv<float>(*d, s);
-  }
-  DVIE_RETURN_LAUNCH();
-}
 
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->g && d->x && d->ws, "wgrad: null pointer");
