@@ -132,7 +132,7 @@ _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, 
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, 100: WarpDesc}
 
 EXPORTS = [
-    "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
+    "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
     "dvie_ew", "dvie_loss", "dvie_loss_partial_count", "dvie_loss_ws_floats", "dvie_warp_fwd",
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error",
@@ -172,6 +172,9 @@ def load():
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]
+        for name in ("dvie_wgrad_splits_hint", "dvie_wgrad_slabs"):
+            getattr(lib, name).argtypes = [vp]
+            getattr(lib, name).restype = i32
         lib.dvie_run_ops.argtypes = [vp, i32, vp]
         lib.dvie_loss_partial_count.argtypes = [vp]
         lib.dvie_loss_partial_count.restype = ctypes.c_size_t

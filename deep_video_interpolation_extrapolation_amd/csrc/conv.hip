@@ -350,7 +350,17 @@ __global__ void pack_kernel(const dvie_pack_desc* __restrict__ descs) {
 
 using namespace dvie;
 
+namespace dvie {
+int wgrad_halo_splits(const dvie_wgrad_desc& p);  // wgrad_halo.hip
+int wgrad_halo_slabs(const dvie_wgrad_desc& p);
+bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s);
+}  // namespace dvie
+
 extern "C" {
+
+int dvie_wgrad_splits_hint(const dvie_wgrad_desc* d) { return d ? wgrad_halo_splits(*d) : 0; }
+
+int dvie_wgrad_slabs(const dvie_wgrad_desc* d) { return d ? wgrad_halo_slabs(*d) : 0; }
 
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->g && d->x && d->ws, "wgrad: null pointer");
@@ -364,6 +374,7 @@ int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   chunk = (chunk + bkp - 1) / bkp * bkp;
   dim3 grid((unsigned)d->splits, (unsigned)(((d->cout + 63) / 64) * ((d->c + 63) / 64)), (unsigned)(d->th * d->tw));
   hipStream_t s = (hipStream_t)stream;
+  if (wgrad_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();
   if (d->dtype == DVIE_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, *d, chunk);
   else

@@ -360,6 +360,8 @@ static void dispatch_conv(const dvie_conv_desc& p, hipStream_t s) {
   }
 }
 
+bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_halo.hip
+
 }  // namespace dvie
 
 using namespace dvie;
@@ -384,6 +386,7 @@ extern "C" int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
   const unsigned long long wb = (unsigned long long)d->cout * d->kpad * es;
   DVIE_CHECK_ARG(xb < 0xFFFFFF00ull && wb < 0xFFFFFF00ull, "conv: operand exceeds the 4 GiB buffer range");
   hipStream_t s = (hipStream_t)stream;
+  if (conv_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();
   if (d->dtype == DVIE_BF16)
     dispatch_conv<bf16_t>(*d, s);
   else {

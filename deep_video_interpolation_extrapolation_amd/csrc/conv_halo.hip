@@ -1,0 +1,531 @@
+// Halo-tile implicit-GEMM convolution for gfx950, bf16 (v3): stride-1 convolutions with a
+// 1x1 or 3x3 tap grid whose output placement is the identity — every 3x3/1x1 forward conv
+// of HRNet/VGG and the data gradient of the stride-1 ones (a 3x3 conv over the output
+// gradient with flipped weights).
+//
+// Why a halo tile: the per-tap implicit GEMM (conv_fwd.hip) gathers every input pixel
+// once per tap, i.e. 9x for a 3x3 conv, from L2 into LDS.  Here a workgroup owns PR
+// output rows x 64 output columns; it stages the input halo of that tile, (PR+TH-1) x
+// (64+TW-1) pixels x 64 channels, ONCE per 64-channel chunk and every tap reads its B
+// fragments from that image at a row/column shift.  Only the weights are streamed per
+// tap (BC rows x 128 B).
+//
+// * LDS images use a 144-byte row pitch (8 data slots + 1 pad slot of 16 B): the 16-lane
+//   groups of ds_read_b128 then hit 16 distinct slots for any 16 distinct rows mod 16, so
+//   the tap-shifted reads are conflict-free and every fragment address is the lane's base
+//   plus a compile-time immediate (no per-tap address arithmetic).
+// * Staging is LDS-DMA (buffer_load_dwordx4 ... lds): 64 lanes fill 64 consecutive slots;
+//   each lane's source offset is precomputed once per workgroup.  Pad slots and taps that
+//   fall outside the image carry an out-of-range offset and land as zeros (conv padding).
+//   The chunk offset is folded into the buffer resource's base, so the precomputed
+//   offsets stay valid for every chunk.
+// * Pipeline: one step = (chunk, tap).  Step s+1's weight tile and a 1/NT share of the
+//   NEXT chunk's halo are issued before the MFMAs of step s; one vmcnt(0)+barrier per step.
+// * MFMA v_mfma_f32_32x32x16_bf16; a wave owns 32*TM output channels x TNR output rows of
+//   64 pixels.  Epilogue through LDS as in conv_fwd.hip (coalesced 16-B row chunks, fused
+//   bias / residual / accumulate / activation / activation-derivative).
+//
+// Reference ops replaced: nn.Conv2d forward / backward-data (nets/HRNet.py, nets/vgg.py).
+#include <stdlib.h>
+#include <string.h>
+
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+namespace dvie {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
+}
+
+__device__ __forceinline__ int xcd_remap3(int b, int nb) {
+  const int g = b & 7, i = b >> 3;
+  const int q = nb >> 3, r = nb & 7;
+  const int start = g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q;
+  return start + i;
+}
+
+__device__ __forceinline__ void act_apply(float* v, int n, int act, float alpha) {
+  if (act == DVIE_ACT_LRELU) {
+    for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : v[k] * alpha;
+  } else if (act == DVIE_ACT_RELU) {
+    for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+  } else if (act == DVIE_ACT_ELU) {
+    for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : expm1f(v[k]);
+  }
+}
+
+__device__ __forceinline__ void dact_apply(float* v, const float* z, int n, int dact, float alpha) {
+  if (dact == DVIE_ACT_LRELU) {
+    for (int k = 0; k < n; ++k) v[k] *= z[k] > 0.f ? 1.f : alpha;
+  } else if (dact == DVIE_ACT_RELU) {
+    for (int k = 0; k < n; ++k) v[k] = z[k] > 0.f ? v[k] : 0.f;
+  } else if (dact == DVIE_ACT_ELU) {
+    for (int k = 0; k < n; ++k) v[k] *= z[k] > 0.f ? 1.f : z[k] + 1.f;
+  }
+}
+
+template <int TM, int WC, int WP, int TH, int TW>
+struct HaloCfg {
+  static constexpr int NW = WC * WP;               // waves per workgroup
+  static constexpr int NTH = NW * 64;
+  static constexpr int BC = 32 * TM * WC;          // output channels per tile
+  static constexpr int PR = WP;                    // output rows per tile (one per row-wave)
+  static constexpr int NT = TH * TW;               // taps
+  static constexpr int HR = PR + TH - 1;           // halo rows
+  static constexpr int HWD = 64 + TW - 1;          // halo columns
+  static constexpr int PITCH = 144;                // bytes per LDS row (8 data + 1 pad slot)
+  static constexpr int HSLOTS = HR * HWD * 9;
+  static constexpr int NHI = ((HSLOTS + 63) / 64 + NW - 1) / NW * NW;  // DMA pieces per halo image
+  static constexpr int NHQ = NHI / NW;             // pieces per wave (exact)
+  static constexpr int HSZ = NHI * 1024;
+  static constexpr int NH = NT > 1 ? 2 : 3;        // halo buffers
+  // weight tile: BC rows x 128 B, XOR-swizzled 16-B chunks (rows are read at fixed offsets,
+  // so the swizzle costs no per-step address arithmetic); BC/8 DMA pieces
+  static constexpr int NAI = BC / 8;
+  static constexpr int NAQ = (NAI + NW - 1) / NW;  // pieces per wave (upper bound)
+  static constexpr int ASZ = BC * 128;
+  static constexpr int NA = 3;                     // weight buffers (two steps of look-ahead)
+  static constexpr int SMEM = NH * HSZ + NA * ASZ;
+  // NT > 1: the next job's halo is issued in shares during taps 0..NT-2 of the current job
+  static constexpr int SPREAD = NT > 1 ? NT - 1 : 1;
+  __host__ __device__ static constexpr int q0(int t) { return t >= SPREAD ? NHQ : t * NHQ / SPREAD; }
+  __host__ __device__ static constexpr int q1(int t) { return t >= SPREAD ? NHQ : (t + 1) * NHQ / SPREAD; }
+};
+
+// s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their maxima)
+#define DVIE_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: DVIE_VMCNT(0); break;
+    case 1: DVIE_VMCNT(1); break;
+    case 2: DVIE_VMCNT(2); break;
+    case 3: DVIE_VMCNT(3); break;
+    case 4: DVIE_VMCNT(4); break;
+    case 5: DVIE_VMCNT(5); break;
+    case 6: DVIE_VMCNT(6); break;
+    case 7: DVIE_VMCNT(7); break;
+    case 8: DVIE_VMCNT(8); break;
+    case 9: DVIE_VMCNT(9); break;
+    case 10: DVIE_VMCNT(10); break;
+    case 11: DVIE_VMCNT(11); break;
+    case 12: DVIE_VMCNT(12); break;
+    case 13: DVIE_VMCNT(13); break;
+    case 14: DVIE_VMCNT(14); break;
+    case 15: DVIE_VMCNT(15); break;
+    case 16: DVIE_VMCNT(16); break;
+    case 17: DVIE_VMCNT(17); break;
+    case 18: DVIE_VMCNT(18); break;
+    case 19: DVIE_VMCNT(19); break;
+    case 20: DVIE_VMCNT(20); break;
+    default: DVIE_VMCNT(0); break;
+  }
+}
+
+struct JobInfo {
+  int valid, k, c0, n, y0, x0;
+};
+
+template <int TM, int WC, int WP, int TH, int TW, bool OUTF32>
+__global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_desc p, int n_ct, int n_tiles,
+                                                                 int tiles_x, int tiles_y, int persistent) {
+  typedef HaloCfg<TM, WC, WP, TH, TW> C;
+  constexpr int NW = C::NW;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave / WP, wp = wave % WP;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nchunks = (p.c + 63) >> 6;  // c < 64: one zero-padded chunk
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // ---- tiles of this workgroup: one (remapped) tile, or an XCD-local strided range ----
+  int tile0, tile_end, tile_step;
+  if (!persistent) {
+    tile0 = xcd_remap3(blockIdx.x, n_tiles);
+    tile_end = tile0 + 1;
+    tile_step = 1;
+  } else {
+    const int G = gridDim.x, g = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int nbg = G / 8 + (g < G % 8 ? 1 : 0);
+    const int q = n_tiles / 8, r = n_tiles % 8;
+    const int ts = g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q;
+    tile0 = ts + j;
+    tile_end = ts + q + (g < r ? 1 : 0);
+    tile_step = nbg;
+  }
+  if (tile0 >= tile_end) return;
+
+  // job j of this workgroup = (its tile j / nchunks, chunk j % nchunks)
+  auto job = [&](int j) {
+    JobInfo J;
+    const int tl = j / nchunks;
+    J.k = j - tl * nchunks;
+    const int t = tile0 + tl * tile_step;
+    J.valid = t < tile_end;
+    J.c0 = (t % n_ct) * C::BC;
+    int pt = t / n_ct;
+    J.x0 = (pt % tiles_x) * 64;
+    pt /= tiles_x;
+    J.y0 = (pt % tiles_y) * C::PR;
+    J.n = pt / tiles_y;
+    return J;
+  };
+
+  // ---- per-lane DMA geometry (tile independent) ----
+  int hgeo[C::NHQ];
+#pragma unroll
+  for (int q = 0; q < C::NHQ; ++q) {
+    const int slot = (wave + NW * q) * 64 + lane;
+    const int hr = slot / 9, cs = slot - 9 * (slot / 9);
+    const int hy = hr / C::HWD, hx = hr - (hr / C::HWD) * C::HWD;
+    hgeo[q] = (cs < 8 && cs * 8 < p.c && hr < C::HR * C::HWD) ? (hy << 16) | (hx << 4) | cs : -1;
+  }
+  // weight DMA: lane fills chunk (lane & 7) of row 8*piece + (lane >> 3) with source chunk
+  // (lane & 7) ^ swz(row)
+  unsigned aoff[C::NAQ];
+#pragma unroll
+  for (int q = 0; q < C::NAQ; ++q) {
+    const int row = (wave + NW * q) * 8 + (lane >> 3);
+    const int cs = (lane & 7) ^ ((row >> 1) & 7);
+    aoff[q] = cs * 8 < p.c ? (unsigned)row * (unsigned)p.kpad * 2u + cs * 16u : OOB;
+  }
+  const int a_cnt = (C::NAI - wave + NW - 1) / NW;  // pieces this wave issues per weight tile
+  const unsigned xrow = (unsigned)p.x_ld * 2u;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+
+  char* const Hs = smem;
+  char* const As = smem + C::NH * C::HSZ;
+
+  // halo pieces [qa, qb) of job J into halo buffer hb
+  auto halo_issue = [&](const JobInfo& J, int hb, int qa, int qb) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.x + (size_t)J.k * 128), 0, (int)(xbytes - (unsigned long long)J.k * 128), 0x00020000);
+    char* dst = Hs + hb * C::HSZ + wave * 1024;
+    const int ybase = J.y0 + p.dy0, xbase = J.x0 + p.dx0;
+#pragma unroll
+    for (int q = qa; q < qb; ++q) {
+      const int gq = hgeo[q];
+      const int iy = ybase + (gq >> 16), ix = xbase + ((gq >> 4) & 0xFFF);
+      const bool ok = gq >= 0 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw;
+      // (offset kept as a separate statement: with it inline, hipcc's host pass drops the
+      // kernel's launch stub)
+      const unsigned o = ok ? (unsigned)((J.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)(gq & 15) * 16u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * NW * 1024), 16, o, 0, 0, 0);
+    }
+  };
+  // weights of (job J, tap t) into weight buffer ab
+  auto a_issue = [&](const JobInfo& J, int t, int ab) {
+    const unsigned o = (unsigned)((long long)J.c0 * p.kpad + t * p.c + 64 * J.k) * 2u;
+    const int nrec = (int)((unsigned)p.cout * (unsigned)p.kpad * 2u - o);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + o), 0, nrec, 0x00020000);
+    char* dst = As + ab * C::ASZ + wave * 1024;
+#pragma unroll
+    for (int q = 0; q < C::NAQ; ++q) {
+      if (q < a_cnt) {
+        const unsigned ao = aoff[q];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * NW * 1024), 16, ao, 0, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc[TM][2];
+  // A fragment addresses for the 4 k-slices (row r32 of the wave's 32-row blocks, chunk 2s+h)
+  int a_off[4];
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    const int row = wc * 32 * TM + r32;
+    a_off[sl] = row * 128 + (((2 * sl + hh) ^ ((row >> 1) & 7)) << 4);
+  }
+  const int b_base = (wp * C::HWD + r32) * C::PITCH + hh * 16;
+
+  // ---- prologue: job 0 halo (+ job 1 for 1x1), weights of steps 0 and 1 ----
+  {
+    const JobInfo J0 = job(0);
+    halo_issue(J0, 0, 0, C::NHQ);
+    a_issue(J0, 0, 0);
+    if (C::NT > 1) {
+      a_issue(J0, 1, 1);
+    } else {
+      const JobInfo J1 = job(1);
+      if (J1.valid) {
+        a_issue(J1, 0, 1);
+        halo_issue(J1, 1, 0, C::NHQ);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  int sc = 0;  // global step counter (weight ring position)
+  JobInfo J = job(0), J1 = job(1), J2 = C::NT > 1 ? J1 : job(2);
+  for (int j = 0;; ++j) {
+    if (j > 0) {  // slide the job window
+      J = J1;
+      if (C::NT > 1) {
+        J1 = job(j + 1);
+        J2 = J1;
+      } else {
+        J1 = J2;
+        J2 = job(j + 2);
+      }
+    }
+    if (!J.valid) break;
+    const int hb = j % C::NH;
+    if (J.k == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][b][e] = 0.f;
+    }
+    const char* H = Hs + hb * C::HSZ + b_base;
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t, ++sc) {
+      const int ti = t / TW, tj = t % TW;
+      const char* A = As + (sc % C::NA) * C::ASZ;
+      // loads issued in this step: weights of step sc+2, halo of a later job
+      const JobInfo& JA = t + 2 < C::NT ? J : (C::NT > 1 ? J1 : J2);
+      const int ta = t + 2 < C::NT ? t + 2 : (C::NT > 1 ? t + 2 - C::NT : 0);
+      const bool do_a = JA.valid != 0;
+      const bool do_h = C::NT > 1 ? (J1.valid && C::q1(t) > C::q0(t)) : (J2.valid != 0);
+      const int issued = (do_a ? a_cnt : 0) + (do_h ? (C::NT > 1 ? C::q1(t) - C::q0(t) : C::NHQ) : 0);
+
+      i32x4 af[2][TM], bfr[2][2];
+      auto frag_load = [&](int s, int fb) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[fb][i] = *(const i32x4*)(A + a_off[s] + i * 32 * 128);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bfr[fb][b] = *(const i32x4*)(H + (ti * C::HWD + 32 * b + tj) * C::PITCH + s * 32);
+      };
+      frag_load(0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s < 3) frag_load(s + 1, (s + 1) & 1);
+        // DMA issue is spread between the MFMA groups
+        if (s == 0 && do_a) a_issue(JA, ta, (sc + 2) % C::NA);
+        if (s == 1 && do_h) {
+          if (C::NT > 1)
+            halo_issue(J1, (j + 1) % C::NH, C::q0(t), C::q1(t));
+          else
+            halo_issue(J2, (j + 2) % C::NH, 0, C::NHQ);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int fb = s & 1;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[fb][i]),
+                                                                __builtin_bit_cast(bf16x8, bfr[fb][b]), acc[i][b], 0,
+                                                                0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // everything issued before this step has landed (this step's loads may stay in flight)
+      wait_vmcnt(issued);
+      // plain s_barrier: __syncthreads() would add a release fence, i.e. vmcnt(0)
+      __builtin_amdgcn_s_barrier();
+    }
+    if (J.k + 1 < nchunks) continue;
+
+    // ---- epilogue straight from the accumulators ----
+    // permlane32_swap pairs the half-waves so that each lane owns 8 consecutive channels
+    // of one pixel: lane half h ends with channels 16P + 8h .. +7 of pair P.
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float v[2][8];
+#pragma unroll
+        for (int P = 0; P < 2; ++P)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][b][8 * P + e]),
+                                                             __float_as_uint(acc[i][b][8 * P + 4 + e]), false, false);
+            v[P][e] = __uint_as_float(sw[0]);
+            v[P][4 + e] = __uint_as_float(sw[1]);
+          }
+        const int oy = J.y0 + wp, ox = J.x0 + 32 * b + r32;
+        if (oy >= p.oh || ox >= p.ow) continue;
+        // output placement (identity, or a stride phase of the strided data gradient)
+        const long long pix = ((long long)J.n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          const int co = J.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh;
+          if (co >= p.cout) continue;
+          float* w = v[P];
+          if (p.bias) {
+            const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[e] += b0[e];
+              w[4 + e] += b1[e];
+            }
+          }
+          if constexpr (OUTF32) {
+            float* dst = (float*)p.y + pix * p.y_ld + co;
+            if (p.res) {
+              const float* rs = (const float*)p.res + pix * p.res_ld + co;
+              const f32x4 r0 = *(const f32x4*)rs, r1 = *(const f32x4*)(rs + 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[e] += r0[e];
+                w[4 + e] += r1[e];
+              }
+            }
+            if (p.beta) {
+              const f32x4 r0 = *(const f32x4*)dst, r1 = *(const f32x4*)(dst + 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[e] += r0[e];
+                w[4 + e] += r1[e];
+              }
+            }
+            act_apply(w, 8, p.act, p.alpha);
+            if (p.dact) {
+              float z[8];
+              const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                z[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
+                z[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
+              }
+              dact_apply(w, z, 8, p.dact, p.alpha);
+            }
+            *(f32x4*)dst = f32x4{w[0], w[1], w[2], w[3]};
+            *(f32x4*)(dst + 4) = f32x4{w[4], w[5], w[6], w[7]};
+          } else {
+            bf16_t* dst = (bf16_t*)p.y + pix * p.y_ld + co;
+            if (p.res) {
+              const i32x4 tr = *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+                w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+              }
+            }
+            if (p.beta) {
+              const i32x4 tr = *(const i32x4*)dst;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+                w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+              }
+            }
+            act_apply(w, 8, p.act, p.alpha);
+            if (p.dact) {
+              float z[8];
+              const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                z[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
+                z[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
+              }
+              dact_apply(w, z, 8, p.dact, p.alpha);
+            }
+            i32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
+            *(i32x4*)dst = o;
+          }
+        }
+      }
+  }
+}
+
+template <int TM, int WC, int WP, int TH, int TW>
+static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
+  typedef HaloCfg<TM, WC, WP, TH, TW> C;
+  if constexpr (C::SMEM > 163840) {
+    return false;
+  } else {
+    const int n_ct = (p.cout + C::BC - 1) / C::BC;
+    const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + C::PR - 1) / C::PR;
+    const long long nt = (long long)n_ct * tiles_x * tiles_y * p.n;
+    if (nt >= (1LL << 30)) return false;
+    const int n_tiles = (int)nt;
+    const int per_cu = 163840 / C::SMEM;
+    const int cap = 256 * (per_cu > 2 ? 2 : per_cu);
+    const int persistent = n_tiles > cap ? 1 : 0;
+    const int grid = persistent ? cap : n_tiles;
+    if (p.out_f32)
+      hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
+                         n_tiles, tiles_x, tiles_y, persistent);
+    else
+      hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, false>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
+                         n_tiles, tiles_x, tiles_y, persistent);
+    return true;
+  }
+}
+
+// tile configurations: id -> (TM, WC, WP): BC = 32*TM*WC output channels x WP rows x 64 pixels,
+// WC*WP waves
+template <int TH, int TW>
+static bool launch_cfg(int cfg, const dvie_conv_desc& p, hipStream_t s) {
+  switch (cfg) {
+    case 0: return try_halo<2, 1, 4, TH, TW>(p, s);  // 64 co x 4 rows, 4 waves
+    case 1: return try_halo<2, 2, 2, TH, TW>(p, s);  // 128 co x 2 rows, 4 waves
+    case 2: return try_halo<1, 1, 4, TH, TW>(p, s);  // 32 co x 4 rows, 4 waves
+    case 3: return try_halo<1, 2, 4, TH, TW>(p, s);  // 64 co x 4 rows, 8 waves
+    case 4: return try_halo<2, 2, 4, TH, TW>(p, s);  // 128 co x 4 rows, 8 waves
+    case 5: return try_halo<1, 4, 2, TH, TW>(p, s);  // 128 co x 2 rows, 8 waves
+    case 6: return try_halo<1, 1, 8, TH, TW>(p, s);  // 32 co x 8 rows, 8 waves
+    case 7: return try_halo<2, 1, 8, TH, TW>(p, s);  // 64 co x 8 rows, 8 waves
+  }
+  return false;
+}
+
+template <int TH, int TW>
+static bool launch_cfg2(int cfg, const dvie_conv_desc& p, hipStream_t s) {
+  return cfg == 3 ? try_halo<1, 2, 4, TH, TW>(p, s) : try_halo<2, 2, 4, TH, TW>(p, s);
+}
+
+static int env_cfg() {
+  // tuning override (read per launch so a tuner can sweep it in one process):
+  // -1 = per-tap kernel (conv_fwd.hip), 0..4 = halo configuration, unset = automatic
+  const char* e = getenv("DVIE_CONV_CFG");
+  return e && *e ? atoi(e) : -3;
+}
+
+// Returns true when the halo kernel took the launch.
+bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
+  if (p.dtype != DVIE_BF16) return false;
+  if (p.sy != 1 || p.sx != 1 || p.ddy != 1 || p.ddx != 1) return false;
+  if (p.osy < 1 || p.osx < 1 || p.ory < 0 || p.orx < 0) return false;
+  if (p.c % 64 != 0 && p.c > 64) return false;  // (c < 64: channels padded with zeros)
+  const bool t1 = p.th == 1 && p.tw == 1, t3 = p.th == 3 && p.tw == 3;
+  const bool t22 = p.th == 2 && p.tw == 2, t12 = p.th == 1 && p.tw == 2, t21 = p.th == 2 && p.tw == 1;
+  if (!t1 && !t3 && !t22 && !t12 && !t21) return false;
+  const unsigned long long pix = (unsigned long long)p.n * p.ih * p.iw;
+  if (pix >= (1ull << 31)) return false;
+  int cfg = env_cfg();
+  if (cfg == -1) return false;
+  if (cfg < 0) {  // measured on MI355X (tools/conv_tune.py): see DESIGN.md
+    if (p.cout <= 32)
+      cfg = 2;
+    else if (p.cout <= 64 || p.cout % 128 != 0)
+      cfg = 3;
+    else if (t1 && p.c == 64)
+      cfg = 5;
+    else
+      cfg = 4;
+  }
+  if (t3) return launch_cfg<3, 3>(cfg, p, s);
+  if (t1) return launch_cfg<1, 1>(cfg, p, s);
+  // stride-2 data-gradient phases: two configurations only
+  const int c2 = p.cout <= 64 || p.cout % 128 != 0 ? 3 : 4;
+  if (t22) return launch_cfg2<2, 2>(c2, p, s);
+  if (t12) return launch_cfg2<1, 2>(c2, p, s);
+  return launch_cfg2<2, 1>(c2, p, s);
+}
+
+}  // namespace dvie

@@ -135,9 +135,12 @@ class ConvLayer:
                 ow = (W - rx + s - 1) // s
                 if oh <= 0 or ow <= 0:
                     continue
-                phases.append(dict(ry=ry, rx=rx, oh=oh, ow=ow, th=len(khs), tw=len(kws), kh0=khs[0], kw0=kws[0],
-                                   dkh=s, dkw=s, dy0=(ry + p - khs[0]) // s, dx0=(rx + p - kws[0]) // s,
-                                   ddy=-1, ddx=-1))
+                # taps ordered by increasing input offset (ddy = ddx = +1): tap i reads
+                # dy0 + i and weight row khs[-1] - i*s
+                th, tw = len(khs), len(kws)
+                phases.append(dict(ry=ry, rx=rx, oh=oh, ow=ow, th=th, tw=tw, kh0=khs[-1], kw0=kws[-1],
+                                   dkh=-s, dkw=-s, dy0=(ry + p - khs[0]) // s - (th - 1),
+                                   dx0=(rx + p - kws[0]) // s - (tw - 1), ddy=1, ddx=1))
         return phases
 
 
@@ -658,16 +661,20 @@ class Plan:
             d.n, d.oh, d.ow, d.cout = nb, out.H, out.W, lay.cout_p
             d.ih, d.iw, d.c, d.sy, d.sx = x.H, x.W, x.c, lay.stride, lay.stride
             d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], 1, 1
-            d.splits, d.dtype = splits, self.dt
-            self.ws_floats = max(self.ws_floats, splits * lay.cout_p * ntap * x.c)
+            d.dtype = self.dt
+            lib = L.load()
+            hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))  # the halo kernel's preferred split
+            d.splits = hint if hint > 0 else splits
+            slabs = lib.dvie_wgrad_slabs(ctypes.byref(d))
+            self.ws_floats = max(self.ws_floats, slabs * lay.cout_p * ntap * x.c)
             o.meta = dict(cls="conv_wgrad", name=lay.name, flops=2.0 * npix * lay.cout * lay.cin * ntap,
                           bytes=float(self.es * (npix * lay.cout + nb * x.H * x.W * lay.cin)
-                                      + 4 * splits * lay.cout_p * ntap * x.c))
+                                      + 4 * slabs * lay.cout_p * ntap * x.c))
             self.bwd.append(o)
             o = self._op(L.OP_WREDUCE)
             r = o.u.wreduce
             r.ws, r.dw, r.cmap = 0, 0, lay.cmap_t.data_ptr()
-            r.splits, r.ws_rows, r.ws_k, r.co_off = splits, lay.cout_p, ntap * x.c, 0
+            r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, ntap * x.c, 0
             r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
             first = lay not in self.wg_first
             r.beta = 0 if first else 1

@@ -101,6 +101,16 @@ typedef struct dvie_wgrad_desc {
 
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream);
 
+/* Split count the library prefers for this weight gradient (0: no preference).  bf16
+ * stride-1 1x1/3x3 convs with c and cout multiples of 64 run a halo-tile kernel that
+ * assigns contiguous ranges of 64-pixel-wide output tiles to splits. */
+int dvie_wgrad_splits_hint(const dvie_wgrad_desc* d);
+
+/* Number of partial slabs ([slabs][cout][taps*c] fp32) dvie_conv2d_wgrad writes for d
+ * (d->splits, or 4*d->splits for the halo kernel's 1x1 case); size `ws` and pass this as
+ * dvie_wreduce_desc.splits. */
+int dvie_wgrad_slabs(const dvie_wgrad_desc* d);
+
 /*
  * dw[co][cmap[j]][kh][kw] (+)= sum_s part[s][co_off + co][t*c + j]  for every packed
  * position j in [0, c) whose source channel cmap[j] >= 0 (identity when cmap is NULL),
