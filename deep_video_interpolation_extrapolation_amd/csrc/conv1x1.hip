@@ -1,0 +1,325 @@
+// 1x1 convolution as a plain GEMM for gfx950, bf16: out[pix][co] = sum_ci x[pix][ci] * w[co][ci]
+// (forward 1x1 convs of HRNet's bottlenecks / fuse layers, and the data gradient of 1x1 convs,
+// including the 1x1 stride phases of strided data gradients through the output placement).
+//
+// A 1x1 conv needs no spatial tiling: a workgroup owns 256 consecutive pixels and BC output
+// channels (BC = 32*TMC up to 256, so 448-channel layers take two column tiles) and walks the
+// input channels in 64-channel K-steps.  Both operands are staged by LDS-DMA into 128-byte
+// XOR-swizzled rows (x tile 256 x 128 B, weight tile BC x 128 B), two stages in flight.
+// Eight waves each own 32 pixels x BC channels (TMC accumulators of 32x32): per 16-deep
+// k-slice a wave reads one pixel fragment and TMC weight fragments and issues TMC MFMAs
+// (v_mfma_f32_32x32x16_bf16).  Epilogue from registers (permlane32 pairing to 16-byte rows)
+// with bias / residual / accumulate / activation / activation-derivative fused.
+//
+// Reference op replaced: nn.Conv2d(kernel_size=1) forward and backward-data (nets/HRNet.py
+// bottleneck conv1/conv3, downsample, fuse and final layers).
+#include <stdlib.h>
+
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+namespace dvie {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_1x1;
+
+#define DVIE_VMCNT1(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
+}
+
+__device__ __forceinline__ void act1(float* v, int act, float alpha) {
+  if (act == DVIE_ACT_LRELU) {
+    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : v[k] * alpha;
+  } else if (act == DVIE_ACT_RELU) {
+    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+  } else if (act == DVIE_ACT_ELU) {
+    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : expm1f(v[k]);
+  }
+}
+
+__device__ __forceinline__ void dact1(float* v, const float* z, int dact, float alpha) {
+  if (dact == DVIE_ACT_LRELU) {
+    for (int k = 0; k < 8; ++k) v[k] *= z[k] > 0.f ? 1.f : alpha;
+  } else if (dact == DVIE_ACT_RELU) {
+    for (int k = 0; k < 8; ++k) v[k] = z[k] > 0.f ? v[k] : 0.f;
+  } else if (dact == DVIE_ACT_ELU) {
+    for (int k = 0; k < 8; ++k) v[k] *= z[k] > 0.f ? 1.f : z[k] + 1.f;
+  }
+}
+
+__device__ __forceinline__ void unpack8(const i32x4 t, float* v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = __uint_as_float(((uint32_t)t[e]) << 16);
+    v[2 * e + 1] = __uint_as_float(((uint32_t)t[e]) & 0xffff0000u);
+  }
+}
+
+template <int TMC, int NS>
+struct G1Cfg {
+  static constexpr int BC = 32 * TMC;
+  static constexpr int BP = 256;
+  static constexpr int XSZ = BP * 128;  // 32 pieces
+  static constexpr int WSZ = BC * 128;  // BC/8 pieces
+  static constexpr int STAGE = XSZ + WSZ;
+  static constexpr int SMEM = NS * STAGE;  // NS stages: NS-1 K-steps in flight
+  static constexpr int XQ = BP / 8 / 8;           // x pieces per wave (8 waves)
+  static constexpr int WQ = (BC / 8 + 7) / 8;     // weight pieces per wave (upper bound)
+};
+
+template <int TMC, int NS, bool OUTF32>
+__global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, int n_ct, int n_tiles) {
+  typedef G1Cfg<TMC, NS> C;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // tile: co tile fastest (consecutive workgroups share the pixel tile in L2), XCD-contiguous
+  const int g = blockIdx.x & 7, i8 = blockIdx.x >> 3;
+  const int q8 = n_tiles >> 3, r8 = n_tiles & 7;
+  const int bid = (g < r8 ? g * (q8 + 1) : r8 * (q8 + 1) + (g - r8) * q8) + i8;
+  const int c0 = (bid % n_ct) * C::BC;
+  const int p0 = (bid / n_ct) * C::BP;
+  const int npix = p.n * p.oh * p.ow;
+  const int nk = (p.c + 63) >> 6;
+
+  // DMA lane geometry: piece = 8 rows x 128 B; lane -> row 8*piece + (lane>>3), LDS chunk
+  // (lane & 7) holding source chunk (lane & 7) ^ swz(row), swz(row) = (row >> 1) & 7
+  const int lrow = lane >> 3, lch = lane & 7;
+  unsigned xo[C::XQ];
+#pragma unroll
+  for (int q = 0; q < C::XQ; ++q) {
+    const int row = (wave + 8 * q) * 8 + lrow;
+    const int cs = lch ^ ((row >> 1) & 7);
+    xo[q] = (p0 + row < npix) ? (unsigned)(p0 + row) * (unsigned)p.x_ld * 2u + cs * 16u : OOB;
+    if (cs * 8 >= p.c) xo[q] = OOB;  // (c < 64: channel padding)
+  }
+  unsigned wo[C::WQ];
+#pragma unroll
+  for (int q = 0; q < C::WQ; ++q) {
+    const int row = (wave + 8 * q) * 8 + lrow;
+    const int cs = lch ^ ((row >> 1) & 7);
+    wo[q] = (row < C::BC && cs * 8 < p.c) ? (unsigned)row * (unsigned)p.kpad * 2u + cs * 16u : OOB;
+  }
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const unsigned wbytes = (unsigned)p.cout * (unsigned)p.kpad * 2u;
+
+  auto stage = [&](int k, int sb) {
+    char* X = smem + sb * C::STAGE;
+    char* W = X + C::XSZ;
+    // K-step k: channels 64k .. 64k+63 (chunks past c land as zeros: range check below)
+    const int xr = (int)(xbytes - (unsigned long long)k * 128);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)k * 128), 0, xr, 0x00020000);
+    const unsigned wb = (unsigned)(c0 * p.kpad + 64 * k) * 2u;
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + wb), 0, (int)(wbytes - wb), 0x00020000);
+    const int cvalid = p.c - 64 * k;  // channels of this K-step that exist
+#pragma unroll
+    for (int q = 0; q < C::XQ; ++q) {
+      const int row = (wave + 8 * q) * 8 + lrow;
+      const int cs = lch ^ ((row >> 1) & 7);
+      const unsigned o = cs * 8 < cvalid ? xo[q] : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_1x1)(X + (wave + 8 * q) * 1024), 16, o, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < C::WQ; ++q) {
+      if (wave + 8 * q < C::BC / 8) {
+        const int row = (wave + 8 * q) * 8 + lrow;
+        const int cs = lch ^ ((row >> 1) & 7);
+        const unsigned o = cs * 8 < cvalid ? wo[q] : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_1x1)(W + (wave + 8 * q) * 1024), 16, o, 0, 0, 0);
+      }
+    }
+  };
+
+  // fragment addresses: pixel row = wave*32 + r32 (B operand), weight rows 32*j + r32 (A);
+  // k-slice s uses chunk 2s + h
+  int xf[4], wf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int prow = wave * 32 + r32;
+    xf[s] = prow * 128 + (((2 * s + hh) ^ ((prow >> 1) & 7)) << 4);
+    wf[s] = r32 * 128 + (((2 * s + hh) ^ ((r32 >> 1) & 7)) << 4);  // (+ 32*j rows: same swizzle)
+  }
+
+  f32x16 acc[TMC];
+#pragma unroll
+  for (int j = 0; j < TMC; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  // prologue: K-steps 0 .. NS-2 in flight
+#pragma unroll
+  for (int k = 0; k < (NS > 1 ? NS - 1 : 1); ++k)
+    if (k < nk) stage(k, k);
+  for (int k = 0; k < nk; ++k) {
+    const int sb = k % NS;
+    // stage k has landed for every wave: this wave's own pieces by the counted wait (stage
+    // k+1, issued after it, may stay in flight), the other waves' by the barrier
+    if constexpr (NS == 3) {
+      constexpr int P_HI = C::XQ + C::WQ, P_LO = C::XQ + C::WQ - 1;  // pieces per wave per stage
+      if (k + 1 < nk) {
+        if (wave + 8 * (C::WQ - 1) < C::BC / 8)
+          DVIE_VMCNT1(P_HI);
+        else
+          DVIE_VMCNT1(P_LO);
+      } else {
+        __builtin_amdgcn_s_waitcnt(0);
+      }
+    } else {
+      static_assert(NS <= 2, "NS > 3 needs a deeper wait table");
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    __builtin_amdgcn_s_barrier();
+    if (NS > 1 && k + NS - 1 < nk) stage(k + NS - 1, (k + NS - 1) % NS);
+    const char* X = smem + sb * C::STAGE;
+    const char* W = X + C::XSZ;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const i32x4 b = *(const i32x4*)(X + xf[s]);
+      i32x4 a[TMC];
+#pragma unroll
+      for (int j = 0; j < TMC; ++j) a[j] = *(const i32x4*)(W + wf[s] + j * 32 * 128);
+#pragma unroll
+      for (int j = 0; j < TMC; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[j]), __builtin_bit_cast(bf16x8, b),
+                                                         acc[j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane owns pixel wave*32 + r32; after permlane32 pairing, lane half h holds
+  // channels 16P + 8h .. +7 of pair P of each 32-channel accumulator
+  const int pix = p0 + wave * 32 + r32;
+  float v[TMC][2][8];
+#pragma unroll
+  for (int j = 0; j < TMC; ++j)
+#pragma unroll
+    for (int P = 0; P < 2; ++P)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[j][8 * P + e]),
+                                                         __float_as_uint(acc[j][8 * P + 4 + e]), false, false);
+        v[j][P][e] = __uint_as_float(sw[0]);
+        v[j][P][4 + e] = __uint_as_float(sw[1]);
+      }
+  if (pix >= npix) return;
+  long long yp = pix;
+  if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) {
+    const int hw = p.oh * p.ow;
+    const int n = pix / hw, r = pix - n * hw;
+    const int oy = r / p.ow, ox = r - oy * p.ow;
+    yp = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+  }
+#pragma unroll
+  for (int j = 0; j < TMC; ++j)
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      const int co = c0 + 32 * j + 16 * P + 8 * hh;
+      if (co >= p.cout) continue;
+      float* w = v[j][P];
+      if (p.bias) {
+        const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[e] += b0[e];
+          w[4 + e] += b1[e];
+        }
+      }
+      if constexpr (OUTF32) {
+        float* dst = (float*)p.y + yp * p.y_ld + co;
+        if (p.res) {
+          const float* rs = (const float*)p.res + yp * p.res_ld + co;
+          const f32x4 r0 = *(const f32x4*)rs, r1 = *(const f32x4*)(rs + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            w[e] += r0[e];
+            w[4 + e] += r1[e];
+          }
+        }
+        if (p.beta) {
+          const f32x4 r0 = *(const f32x4*)dst, r1 = *(const f32x4*)(dst + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            w[e] += r0[e];
+            w[4 + e] += r1[e];
+          }
+        }
+        act1(w, p.act, p.alpha);
+        if (p.dact) {
+          float z[8];
+          unpack8(*(const i32x4*)((const bf16_t*)p.z + yp * p.z_ld + co), z);
+          dact1(w, z, p.dact, p.alpha);
+        }
+        *(f32x4*)dst = f32x4{w[0], w[1], w[2], w[3]};
+        *(f32x4*)(dst + 4) = f32x4{w[4], w[5], w[6], w[7]};
+      } else {
+        bf16_t* dst = (bf16_t*)p.y + yp * p.y_ld + co;
+        float t[8];
+        if (p.res) {
+          unpack8(*(const i32x4*)((const bf16_t*)p.res + yp * p.res_ld + co), t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] += t[e];
+        }
+        if (p.beta) {
+          unpack8(*(const i32x4*)dst, t);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w[e] += t[e];
+        }
+        act1(w, p.act, p.alpha);
+        if (p.dact) {
+          unpack8(*(const i32x4*)((const bf16_t*)p.z + yp * p.z_ld + co), t);
+          dact1(w, t, p.dact, p.alpha);
+        }
+        i32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (int)pk_bf16(w[2 * e], w[2 * e + 1]);
+        *(i32x4*)dst = o;
+      }
+    }
+}
+
+template <int TMC, int NS>
+static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
+  typedef G1Cfg<TMC, NS> C;
+  const int npix = p.n * p.oh * p.ow;
+  const int n_ct = (p.cout + C::BC - 1) / C::BC;
+  const int n_tiles = n_ct * ((npix + C::BP - 1) / C::BP);
+  if (p.out_f32)
+    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, true>), dim3(n_tiles), dim3(512), 0, s, p, n_ct, n_tiles);
+  else
+    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, false>), dim3(n_tiles), dim3(512), 0, s, p, n_ct, n_tiles);
+}
+
+// Returns true when the 1x1 GEMM kernel took the launch.
+bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
+  if (p.dtype != DVIE_BF16 || p.th != 1 || p.tw != 1) return false;
+  if (p.sy != 1 || p.sx != 1 || p.dy0 != 0 || p.dx0 != 0 || p.ih != p.oh || p.iw != p.ow) return false;
+  if (p.osy < 1 || p.osx < 1 || p.ory < 0 || p.orx < 0) return false;
+  if (p.c % 64 != 0 && p.c > 64) return false;
+  if ((long long)p.n * p.oh * p.ow >= (1LL << 31)) return false;
+  const char* e = getenv("DVIE_CONV_CFG");
+  int cfg = e && *e ? atoi(e) : -3;
+  if (cfg >= 0 && cfg < 100) return false;  // tuning override forces the halo / per-tap kernels
+  const int cout = p.cout;
+  const bool one = p.c <= 64;  // a single K-step: one stage, several workgroups per CU
+  if (cfg < 0) cfg = cout <= 64 ? 100 : (cout <= 128 || one) ? 101 : 102;
+  switch (cfg) {
+    case 100: one ? launch_1x1<2, 1>(p, s) : launch_1x1<2, 3>(p, s); break;
+    case 101: one ? launch_1x1<4, 1>(p, s) : launch_1x1<4, 3>(p, s); break;
+    case 102: one ? launch_1x1<7, 1>(p, s) : launch_1x1<7, 2>(p, s); break;
+    case 103: one ? launch_1x1<8, 1>(p, s) : launch_1x1<8, 2>(p, s); break;
+    case 104: one ? launch_1x1<4, 1>(p, s) : launch_1x1<4, 2>(p, s); break;
+    default: return false;
+  }
+  return true;
+}
+
+}  // namespace dvie

@@ -361,6 +361,7 @@ static void dispatch_conv(const dvie_conv_desc& p, hipStream_t s) {
 }
 
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_halo.hip
+bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s);    // conv1x1.hip
 
 }  // namespace dvie
 
@@ -386,6 +387,7 @@ extern "C" int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
   const unsigned long long wb = (unsigned long long)d->cout * d->kpad * es;
   DVIE_CHECK_ARG(xb < 0xFFFFFF00ull && wb < 0xFFFFFF00ull, "conv: operand exceeds the 4 GiB buffer range");
   hipStream_t s = (hipStream_t)stream;
+  if (conv1x1_launch(*d, s)) DVIE_RETURN_LAUNCH();
   if (conv_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();
   if (d->dtype == DVIE_BF16)
     dispatch_conv<bf16_t>(*d, s);

@@ -128,7 +128,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 }
 
 struct JobInfo {
-  int valid, k, c0, n, y0, x0;
+  int valid, t, k, c0, n, y0, x0;
 };
 
 template <int TM, int WC, int WP, int TH, int TW, bool OUTF32>
@@ -163,12 +163,11 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   }
   if (tile0 >= tile_end) return;
 
-  // job j of this workgroup = (its tile j / nchunks, chunk j % nchunks)
-  auto job = [&](int j) {
+  // jobs of this workgroup: (tile, chunk) in order; the tile is decoded only when it changes
+  auto tile_job = [&](int t) {
     JobInfo J;
-    const int tl = j / nchunks;
-    J.k = j - tl * nchunks;
-    const int t = tile0 + tl * tile_step;
+    J.t = t;
+    J.k = 0;
     J.valid = t < tile_end;
     J.c0 = (t % n_ct) * C::BC;
     int pt = t / n_ct;
@@ -177,6 +176,14 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
     J.y0 = (pt % tiles_y) * C::PR;
     J.n = pt / tiles_y;
     return J;
+  };
+  auto next_job = [&](const JobInfo& J) {
+    if (J.k + 1 < nchunks) {
+      JobInfo N = J;
+      N.k = J.k + 1;
+      return N;
+    }
+    return tile_job(J.t + tile_step);
   };
 
   // ---- per-lane DMA geometry (tile independent) ----
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
     const int cs = (lane & 7) ^ ((row >> 1) & 7);
     aoff[q] = cs * 8 < p.c ? (unsigned)row * (unsigned)p.kpad * 2u + cs * 16u : OOB;
   }
-  const int a_cnt = (C::NAI - wave + NW - 1) / NW;  // pieces this wave issues per weight tile
+  static_assert(C::NAI % NW == 0, "every wave issues the same number of weight pieces");
   const unsigned xrow = (unsigned)p.x_ld * 2u;
   const unsigned long long xbytes =
       ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
@@ -206,9 +213,12 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   char* const As = smem + C::NH * C::HSZ;
 
   // halo pieces [qa, qb) of job J into halo buffer hb
+  // (a job past the end still issues its pieces, with an empty buffer range: they land as
+  // zeros in a buffer nobody reads, and every wave's vmcnt bookkeeping stays compile-time)
   auto halo_issue = [&](const JobInfo& J, int hb, int qa, int qb) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)p.x + (size_t)J.k * 128), 0, (int)(xbytes - (unsigned long long)J.k * 128), 0x00020000);
+    const int nrec = J.valid ? (int)(xbytes - (unsigned long long)J.k * 128) : 0;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)J.k * 128), 0, nrec, 0x00020000);
     char* dst = Hs + hb * C::HSZ + wave * 1024;
     const int ybase = J.y0 + p.dy0, xbase = J.x0 + p.dx0;
 #pragma unroll
@@ -225,15 +235,13 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   // weights of (job J, tap t) into weight buffer ab
   auto a_issue = [&](const JobInfo& J, int t, int ab) {
     const unsigned o = (unsigned)((long long)J.c0 * p.kpad + t * p.c + 64 * J.k) * 2u;
-    const int nrec = (int)((unsigned)p.cout * (unsigned)p.kpad * 2u - o);
+    const int nrec = J.valid ? (int)((unsigned)p.cout * (unsigned)p.kpad * 2u - o) : 0;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + o), 0, nrec, 0x00020000);
     char* dst = As + ab * C::ASZ + wave * 1024;
 #pragma unroll
     for (int q = 0; q < C::NAQ; ++q) {
-      if (q < a_cnt) {
-        const unsigned ao = aoff[q];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * NW * 1024), 16, ao, 0, 0, 0);
-      }
+      const unsigned ao = aoff[q];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * NW * 1024), 16, ao, 0, 0, 0);
     }
   };
 
@@ -249,33 +257,33 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
 
   // ---- prologue: job 0 halo (+ job 1 for 1x1), weights of steps 0 and 1 ----
   {
-    const JobInfo J0 = job(0);
+    const JobInfo J0 = tile_job(tile0);
     halo_issue(J0, 0, 0, C::NHQ);
     a_issue(J0, 0, 0);
     if (C::NT > 1) {
       a_issue(J0, 1, 1);
     } else {
-      const JobInfo J1 = job(1);
-      if (J1.valid) {
-        a_issue(J1, 0, 1);
-        halo_issue(J1, 1, 0, C::NHQ);
-      }
+      const JobInfo J1 = next_job(J0);
+      a_issue(J1, 0, 1);
+      halo_issue(J1, 1, 0, C::NHQ);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
 
   int sc = 0;  // global step counter (weight ring position)
-  JobInfo J = job(0), J1 = job(1), J2 = C::NT > 1 ? J1 : job(2);
+  JobInfo J = tile_job(tile0);
+  JobInfo J1 = next_job(J);
+  JobInfo J2 = C::NT > 1 ? J1 : next_job(J1);
   for (int j = 0;; ++j) {
     if (j > 0) {  // slide the job window
       J = J1;
       if (C::NT > 1) {
-        J1 = job(j + 1);
+        J1 = next_job(J1);
         J2 = J1;
       } else {
         J1 = J2;
-        J2 = job(j + 2);
+        J2 = next_job(J2);
       }
     }
     if (!J.valid) break;
@@ -296,9 +304,9 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
       // loads issued in this step: weights of step sc+2, halo of a later job
       const JobInfo& JA = t + 2 < C::NT ? J : (C::NT > 1 ? J1 : J2);
       const int ta = t + 2 < C::NT ? t + 2 : (C::NT > 1 ? t + 2 - C::NT : 0);
-      const bool do_a = JA.valid != 0;
-      const bool do_h = C::NT > 1 ? (J1.valid && C::q1(t) > C::q0(t)) : (J2.valid != 0);
-      const int issued = (do_a ? a_cnt : 0) + (do_h ? (C::NT > 1 ? C::q1(t) - C::q0(t) : C::NHQ) : 0);
+      constexpr bool kNT1 = C::NT == 1;
+      const bool do_h = kNT1 || C::q1(t) > C::q0(t);
+      const int issued = C::NAQ + (kNT1 ? C::NHQ : C::q1(t) - C::q0(t));
 
       i32x4 af[2][TM], bfr[2][2];
       auto frag_load = [&](int s, int fb) {
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
       for (int s = 0; s < 4; ++s) {
         if (s < 3) frag_load(s + 1, (s + 1) & 1);
         // DMA issue is spread between the MFMA groups
-        if (s == 0 && do_a) a_issue(JA, ta, (sc + 2) % C::NA);
+        if (s == 0) a_issue(JA, ta, (sc + 2) % C::NA);
         if (s == 1 && do_h) {
           if (C::NT > 1)
             halo_issue(J1, (j + 1) % C::NH, C::q0(t), C::q1(t));
@@ -512,12 +520,10 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (cfg < 0) {  // measured on MI355X (tools/conv_tune.py): see DESIGN.md
     if (p.cout <= 32)
       cfg = 2;
-    else if (p.cout <= 64 || p.cout % 128 != 0)
-      cfg = 3;
-    else if (t1 && p.c == 64)
-      cfg = 5;
+    else if (t1)  // 1x1: wide weight tiles amortise the per-chunk pixel tile
+      cfg = p.cout <= 64 ? 3 : (p.c <= 64 ? 5 : 4);
     else
-      cfg = 4;
+      cfg = (p.cout <= 64 || p.cout % 128 != 0) ? 3 : 4;
   }
   if (t3) return launch_cfg<3, 3>(cfg, p, s);
   if (t1) return launch_cfg<1, 1>(cfg, p, s);

@@ -2,7 +2,8 @@
 // (align_corners=False), the gather-form adjoint of that upsampling, 2x2 average pooling
 // and its adjoint, copies, feature-L1 sign gradients and NCHW<->NHWC packing.  Every op
 // shares the same epilogue (residual add, accumulate, activation, activation-derivative)
-// so backward contributions fuse into one pass.  Each thread owns 4 channels of one pixel.
+// so backward contributions fuse into one pass.  Each thread owns 8 (bf16, 16-byte
+// accesses) or 4 channels of one pixel; blocks run along one image row.
 //
 // Reference ops replaced: F.interpolate/F.upsample(mode='bilinear') of
 // nets/HRNet.py:219-222,577-580 (+ the sums/LeakyReLU of l.212-225), AvgPool2d of
@@ -31,17 +32,57 @@ __device__ __forceinline__ Lerp lerp_src(int dst, int in_size, int out_size) {
   return r;
 }
 
+// VW-channel vectors (16 B for bf16 x8 / fp32 x4; 8 B for bf16 x4)
+template <typename T, int VW>
+struct VecN;
+template <>
+struct VecN<bf16_t, 8> {
+  __device__ __forceinline__ static void load(const bf16_t* p, float* v) {
+    const i32x4 r = *(const i32x4*)p;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(((uint32_t)r[k]) << 16);
+      v[2 * k + 1] = __uint_as_float(((uint32_t)r[k]) & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, const float* v) {
+    i32x4 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = (int)((uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16));
+    *(i32x4*)p = r;
+  }
+};
 template <typename T>
-__device__ __forceinline__ f32x4 up_sample(const T* __restrict__ s, long long ld, int n, int y, int x, int c, int sh,
-                                           int sw, int h, int w) {
-  if (sh == h && sw == w) return V4<T>::load(s + (((long long)n * sh + y) * sw + x) * ld + c);
+struct VecN<T, 4> {
+  __device__ __forceinline__ static void load(const T* p, float* v) {
+    const f32x4 r = V4<T>::load(p);
+    v[0] = r[0];
+    v[1] = r[1];
+    v[2] = r[2];
+    v[3] = r[3];
+  }
+  __device__ __forceinline__ static void store(T* p, const float* v) { V4<T>::store(p, f32x4{v[0], v[1], v[2], v[3]}); }
+};
+
+template <typename T, int VW>
+__device__ __forceinline__ void up_sample_add(float* v, const T* __restrict__ s, long long ld, int n, int y, int x,
+                                              int c, int sh, int sw, int h, int w) {
+  float t[VW];
+  if (sh == h && sw == w) {
+    VecN<T, VW>::load(s + (((long long)n * sh + y) * sw + x) * ld + c, t);
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] += t[k];
+    return;
+  }
   const Lerp ly = lerp_src(y, sh, h), lx = lerp_src(x, sw, w);
   const long long r0 = ((long long)n * sh + ly.i0) * sw, r1 = ((long long)n * sh + ly.i1) * sw;
-  const f32x4 a = V4<T>::load(s + (r0 + lx.i0) * ld + c);
-  const f32x4 b = V4<T>::load(s + (r0 + lx.i1) * ld + c);
-  const f32x4 cc = V4<T>::load(s + (r1 + lx.i0) * ld + c);
-  const f32x4 d = V4<T>::load(s + (r1 + lx.i1) * ld + c);
-  return ly.l0 * (lx.l0 * a + lx.l1 * b) + ly.l1 * (lx.l0 * cc + lx.l1 * d);
+  float a[VW], b[VW], cc[VW], d[VW];
+  VecN<T, VW>::load(s + (r0 + lx.i0) * ld + c, a);
+  VecN<T, VW>::load(s + (r0 + lx.i1) * ld + c, b);
+  VecN<T, VW>::load(s + (r1 + lx.i0) * ld + c, cc);
+  VecN<T, VW>::load(s + (r1 + lx.i1) * ld + c, d);
+#pragma unroll
+  for (int k = 0; k < VW; ++k) v[k] += ly.l0 * (lx.l0 * a[k] + lx.l1 * b[k]) + ly.l1 * (lx.l0 * cc[k] + lx.l1 * d[k]);
 }
 
 // weight of fine index `f` (fine size `fs`) onto coarse index `cidx` (coarse size `cs`)
@@ -53,117 +94,140 @@ __device__ __forceinline__ float upt_weight(int f, int cidx, int cs, int fs) {
   return wgt;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p) {
-  const int cq = p.c >> 2;
-  const long long total = (long long)p.n * p.h * p.w * cq;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(e % cq);
-    const long long pix = e / cq;
-    const int x = (int)(pix % p.w);
-    const int y = (int)((pix / p.w) % p.h);
-    const int n = (int)(pix / ((long long)p.w * p.h));
-    const int c = q * 4;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    switch (p.op) {
-      case DVIE_EW_FUSE:
-        v = up_sample<T>((const T*)p.src0, p.src_ld0, n, y, x, c, p.sh0, p.sw0, p.h, p.w);
-        if (p.nsrc > 1) v += up_sample<T>((const T*)p.src1, p.src_ld1, n, y, x, c, p.sh1, p.sw1, p.h, p.w);
-        if (p.nsrc > 2) v += up_sample<T>((const T*)p.src2, p.src_ld2, n, y, x, c, p.sh2, p.sw2, p.h, p.w);
-        break;
-      case DVIE_EW_UPT: {
-        // coarse output (y, x) of a (h, w) grid, fine source (sh0, sw0)
-        const T* s = (const T*)p.src0;
-        const float fy = (float)p.sh0 / (float)p.h, fx = (float)p.sw0 / (float)p.w;
-        int ylo = (int)floorf(((float)y - 0.5f) * fy - 0.5f) - 1, yhi = (int)ceilf(((float)y + 1.5f) * fy) + 1;
-        int xlo = (int)floorf(((float)x - 0.5f) * fx - 0.5f) - 1, xhi = (int)ceilf(((float)x + 1.5f) * fx) + 1;
-        if (ylo < 0) ylo = 0;
-        if (xlo < 0) xlo = 0;
-        if (yhi > p.sh0 - 1) yhi = p.sh0 - 1;
-        if (xhi > p.sw0 - 1) xhi = p.sw0 - 1;
-        for (int Y = ylo; Y <= yhi; ++Y) {
-          const float wy = upt_weight(Y, y, p.h, p.sh0);
-          if (wy == 0.f) continue;
-          f32x4 row = f32x4{0.f, 0.f, 0.f, 0.f};
-          for (int X = xlo; X <= xhi; ++X) {
-            const float wx = upt_weight(X, x, p.w, p.sw0);
-            if (wx == 0.f) continue;
-            row += wx * V4<T>::load(s + (((long long)n * p.sh0 + Y) * p.sw0 + X) * p.src_ld0 + c);
-          }
-          v += wy * row;
-        }
-        break;
-      }
-      case DVIE_EW_POOL: {
-        const T* s = (const T*)p.src0;
-        const long long r0 = ((long long)n * p.sh0 + 2 * y) * p.sw0 + 2 * x;
-        const long long r1 = r0 + p.sw0;
-        v = V4<T>::load(s + r0 * p.src_ld0 + c) + V4<T>::load(s + (r0 + 1) * p.src_ld0 + c) +
-            V4<T>::load(s + r1 * p.src_ld0 + c) + V4<T>::load(s + (r1 + 1) * p.src_ld0 + c);
-        v = v / 4.f;
-        break;
-      }
-      case DVIE_EW_POOLT: {
-        const T* s = (const T*)p.src0;
-        v = V4<T>::load(s + (((long long)n * p.sh0 + (y >> 1)) * p.sw0 + (x >> 1)) * p.src_ld0 + c) / 4.f;
-        break;
-      }
-      case DVIE_EW_COPY:
-        v = V4<T>::load((const T*)p.src0 + pix * p.src_ld0 + c);
-        break;
-      case DVIE_EW_L1SIGN: {
-        const f32x4 a = V4<T>::load((const T*)p.src0 + pix * p.src_ld0 + c);
-        const f32x4 b = V4<T>::load((const T*)p.src1 + pix * p.src_ld1 + c);
+// One thread = VW channels of one pixel; blockIdx.y = image row (n, y), so the per-element
+// index math is one 32-bit division by the channel-vector count.
+template <typename T, int VW>
+__global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= p.w * cq) return;
+  const int x = e / cq;
+  const int c = (e - x * cq) * VW;
+  const int row = blockIdx.y;
+  const int n = row / p.h, y = row - (row / p.h) * p.h;
+  const long long pix = (long long)row * p.w + x;
+  float v[VW];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float d = a[k] - b[k];
-          v[k] = d > 0.f ? p.scale : (d < 0.f ? -p.scale : 0.f);
-        }
-        break;
-      }
-      case DVIE_EW_NCHW: {
+  for (int k = 0; k < VW; ++k) v[k] = 0.f;
+  switch (p.op) {
+    case DVIE_EW_FUSE:
+      up_sample_add<T, VW>(v, (const T*)p.src0, p.src_ld0, n, y, x, c, p.sh0, p.sw0, p.h, p.w);
+      if (p.nsrc > 1) up_sample_add<T, VW>(v, (const T*)p.src1, p.src_ld1, n, y, x, c, p.sh1, p.sw1, p.h, p.w);
+      if (p.nsrc > 2) up_sample_add<T, VW>(v, (const T*)p.src2, p.src_ld2, n, y, x, c, p.sh2, p.sw2, p.h, p.w);
+      break;
+    case DVIE_EW_UPT: {
+      // coarse output (y, x) of a (h, w) grid, fine source (sh0, sw0)
+      const T* s = (const T*)p.src0;
+      const float fy = (float)p.sh0 / (float)p.h, fx = (float)p.sw0 / (float)p.w;
+      int ylo = (int)floorf(((float)y - 0.5f) * fy - 0.5f) - 1, yhi = (int)ceilf(((float)y + 1.5f) * fy) + 1;
+      int xlo = (int)floorf(((float)x - 0.5f) * fx - 0.5f) - 1, xhi = (int)ceilf(((float)x + 1.5f) * fx) + 1;
+      if (ylo < 0) ylo = 0;
+      if (xlo < 0) xlo = 0;
+      if (yhi > p.sh0 - 1) yhi = p.sh0 - 1;
+      if (xhi > p.sw0 - 1) xhi = p.sw0 - 1;
+      for (int Y = ylo; Y <= yhi; ++Y) {
+        const float wy = upt_weight(Y, y, p.h, p.sh0);
+        if (wy == 0.f) continue;
+        float rowv[VW];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int ch = c + k;
-          if (ch < p.ext_c) {
-            float t = p.ext[(long long)n * p.sn + (long long)ch * p.sc + (long long)y * p.sh + (long long)x * p.sw];
-            if (p.mean) t = (t - p.mean[ch]) / p.std[ch];
-            v[k] = t;
-          }
-        }
-        break;
-      }
-      case DVIE_EW_TONCHW: {
-        const f32x4 a = V4<T>::load((const T*)p.src0 + pix * p.src_ld0 + c);
+        for (int k = 0; k < VW; ++k) rowv[k] = 0.f;
+        for (int X = xlo; X <= xhi; ++X) {
+          const float wx = upt_weight(X, x, p.w, p.sw0);
+          if (wx == 0.f) continue;
+          float t[VW];
+          VecN<T, VW>::load(s + (((long long)n * p.sh0 + Y) * p.sw0 + X) * p.src_ld0 + c, t);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int ch = c + k;
-          if (ch < p.ext_c) {
-            float* d = p.ext + (long long)n * p.sn + (long long)ch * p.sc + (long long)y * p.sh + (long long)x * p.sw;
-            const float v = p.std ? a[k] / p.std[ch] : a[k];  // adjoint of preprocess_norm
-            *d = p.beta ? *d + v : v;
-          }
+          for (int k = 0; k < VW; ++k) rowv[k] += wx * t[k];
         }
-        continue;
+#pragma unroll
+        for (int k = 0; k < VW; ++k) v[k] += wy * rowv[k];
       }
-      default:
-        break;
+      break;
     }
-    T* yp = (T*)p.y + pix * p.y_ld + c;
-    if (p.res) v += V4<T>::load((const T*)p.res + pix * p.res_ld + c);
-    if (p.beta) v += V4<T>::load(yp);
-    if (p.act) {
+    case DVIE_EW_POOL: {
+      const T* s = (const T*)p.src0;
+      const long long r0 = ((long long)n * p.sh0 + 2 * y) * p.sw0 + 2 * x;
+      const long long r1 = r0 + p.sw0;
+      float a[VW], b[VW], cc[VW], d[VW];
+      VecN<T, VW>::load(s + r0 * p.src_ld0 + c, a);
+      VecN<T, VW>::load(s + (r0 + 1) * p.src_ld0 + c, b);
+      VecN<T, VW>::load(s + r1 * p.src_ld0 + c, cc);
+      VecN<T, VW>::load(s + (r1 + 1) * p.src_ld0 + c, d);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = act_fwd(v[k], p.act, p.alpha);
+      for (int k = 0; k < VW; ++k) v[k] = (a[k] + b[k] + cc[k] + d[k]) / 4.f;
+      break;
     }
-    if (p.dact) {
-      const f32x4 z = V4<T>::load((const T*)p.z + pix * p.z_ld + c);
+    case DVIE_EW_POOLT: {
+      const T* s = (const T*)p.src0;
+      VecN<T, VW>::load(s + (((long long)n * p.sh0 + (y >> 1)) * p.sw0 + (x >> 1)) * p.src_ld0 + c, v);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] *= act_dz(z[k], p.dact, p.alpha);
+      for (int k = 0; k < VW; ++k) v[k] = v[k] / 4.f;
+      break;
     }
-    V4<T>::store(yp, v);
+    case DVIE_EW_COPY:
+      VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, v);
+      break;
+    case DVIE_EW_L1SIGN: {
+      float a[VW], b[VW];
+      VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, a);
+      VecN<T, VW>::load((const T*)p.src1 + pix * p.src_ld1 + c, b);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        const float d = a[k] - b[k];
+        v[k] = d > 0.f ? p.scale : (d < 0.f ? -p.scale : 0.f);
+      }
+      break;
+    }
+    case DVIE_EW_NCHW: {
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        const int ch = c + k;
+        if (ch < p.ext_c) {
+          float t = p.ext[(long long)n * p.sn + (long long)ch * p.sc + (long long)y * p.sh + (long long)x * p.sw];
+          if (p.mean) t = (t - p.mean[ch]) / p.std[ch];
+          v[k] = t;
+        }
+      }
+      break;
+    }
+    case DVIE_EW_TONCHW: {
+      float a[VW];
+      VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, a);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        const int ch = c + k;
+        if (ch < p.ext_c) {
+          float* d = p.ext + (long long)n * p.sn + (long long)ch * p.sc + (long long)y * p.sh + (long long)x * p.sw;
+          const float t = p.std ? a[k] / p.std[ch] : a[k];  // adjoint of preprocess_norm
+          *d = p.beta ? *d + t : t;
+        }
+      }
+      return;
+    }
+    default:
+      break;
   }
+  T* yp = (T*)p.y + pix * p.y_ld + c;
+  float t[VW];
+  if (p.res) {
+    VecN<T, VW>::load((const T*)p.res + pix * p.res_ld + c, t);
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] += t[k];
+  }
+  if (p.beta) {
+    VecN<T, VW>::load(yp, t);
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] += t[k];
+  }
+  if (p.act) {
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] = act_fwd(v[k], p.act, p.alpha);
+  }
+  if (p.dact) {
+    VecN<T, VW>::load((const T*)p.z + pix * p.z_ld + c, t);
+#pragma unroll
+    for (int k = 0; k < VW; ++k) v[k] *= act_dz(t[k], p.dact, p.alpha);
+  }
+  VecN<T, VW>::store(yp, v);
 }
 
 }  // namespace dvie
@@ -178,13 +242,22 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
   if (d->op == DVIE_EW_POOLT) DVIE_CHECK_ARG(d->h == 2 * d->sh0 && d->w == 2 * d->sw0, "ew: poolT shape");
   if (d->op == DVIE_EW_NCHW || d->op == DVIE_EW_TONCHW) DVIE_CHECK_ARG(d->ext != nullptr, "ew: ext");
   if (d->dact) DVIE_CHECK_ARG(d->z != nullptr && d->z_ld % 4 == 0, "ew: z");
-  const long long total = (long long)d->n * d->h * d->w * (d->c / 4);
-  long long blocks = (total + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  DVIE_CHECK_ARG((long long)d->n * d->h < 65536 && (long long)d->w * d->c < (1LL << 30), "ew: grid too large");
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(ew_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, *d);
-  else
-    hipLaunchKernelGGL(ew_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, *d);
+  // 16-byte vectors for bf16 when every operand allows it
+  auto al = [](const void* q, long long ld) { return !q || ((((uintptr_t)q) & 15) == 0 && ld % 8 == 0); };
+  const bool v8 = d->dtype == DVIE_BF16 && d->c % 8 == 0 && al(d->y, d->y_ld) && al(d->src0, d->src_ld0) &&
+                  al(d->src1, d->src_ld1) && al(d->src2, d->src_ld2) && al(d->res, d->res_ld) && al(d->z, d->z_ld);
+  const int vw = v8 ? 8 : 4;
+  const int cq = d->c / vw;
+  const dim3 grid((unsigned)((d->w * cq + 255) / 256), (unsigned)(d->n * d->h));
+  if (d->dtype == DVIE_BF16) {
+    if (v8)
+      hipLaunchKernelGGL((ew_kernel<bf16_t, 8>), grid, dim3(256), 0, s, *d, cq);
+    else
+      hipLaunchKernelGGL((ew_kernel<bf16_t, 4>), grid, dim3(256), 0, s, *d, cq);
+  } else {
+    hipLaunchKernelGGL((ew_kernel<float, 4>), grid, dim3(256), 0, s, *d, cq);
+  }
   DVIE_RETURN_LAUNCH();
 }

@@ -38,33 +38,46 @@ template <int TH, int TW, int PR, int TMO, int TMI>
 struct WgCfg {
   static constexpr int NT = TH * TW;
   static constexpr int BCO = 64 * TMO, BCI = 64 * TMI;  // output / input channels per block
-  static constexpr int HR = PR + TH - 1, HWD = 64 + TW - 1;
+  static constexpr int HR = PR + TH - 1;                // halo rows of one tile
+  static constexpr int XW = TW == 1 ? 64 : 72;          // LDS row pitch of a halo row, in pixels
+  static constexpr int R = HR + PR;                     // ring: current tile + next tile's new rows
   static constexpr int GROWS = PR * 64;
-  static constexpr int XROWS = HR * HWD;
-  static constexpr int GPI = GROWS / 8;               // DMA pieces (8 rows x 128 B) per sub-image
-  static constexpr int XPI = (XROWS + 7) / 8;
-  static constexpr int GSUB = GPI * 1024, XSUB = XPI * 1024;  // one 64-channel sub-image
+  static constexpr int GPI = GROWS / 8;                 // DMA pieces (8 pixels x 128 B) per sub-image
+  static constexpr int XPR = XW / 8;                    // DMA pieces per halo row
+  static constexpr int GSUB = GPI * 1024;               // one 64-channel G sub-image
+  static constexpr int XSUB = R * XW * 128;             // one 64-channel X ring
   static constexpr int GSZ = TMO * GSUB, XSZ = TMI * XSUB;
-  static constexpr int NGP = TMO * GPI, NXP = TMI * XPI;
-  static constexpr int GQ = (NGP + 3) / 4, XQ = (NXP + 3) / 4;
-  static constexpr int BUF = GSZ + XSZ;
-  static constexpr int SMEM = 2 * BUF;
+  static constexpr int SMEM = 2 * GSZ + XSZ;
   static constexpr int NACC = NT * TMO * TMI;
 };
 
+// Tiles walk down a column (ty fastest) so that consecutive tiles of a workgroup share
+// TH-1 halo rows: the input halo lives in a ring of R = HR + PR rows, and each new tile loads
+// only its PR new rows (while the current tile computes) plus its output-gradient tile.
+__device__ __forceinline__ int xcd_chunk(int b, int nb) {
+  // blocks b and b+8 share an XCD under round-robin dispatch: give XCD g a contiguous range
+  const int g = b & 7, i = b >> 3;
+  const int q = nb >> 3, r = nb & 7;
+  return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
+}
+
+// 8 waves: (co half, ci half, row half); the two row halves accumulate separately and write
+// two partial slabs per split.
 template <int TH, int TW, int PR, int TMO, int TMI>
-__global__ __launch_bounds__(256) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
+__global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
                                                          int tiles_x, int tiles_y, int n_tiles) {
   typedef WgCfg<TH, TW, PR, TMO, TMI> C;
+  static_assert(PR % 2 == 0, "row halves");
+  constexpr int NW = 8;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned OOB = 0xFFFFFFF0u;
 
-  // block -> (co block, ci block, split); co/ci blocks fastest so that concurrently running
-  // blocks share their g / x tiles in L2
+  // all (co, ci) pairs of one split run on one XCD, so they share the split's g / x tiles in L2
   const int npair = n_co * n_ci;
-  const int pair = blockIdx.x % npair, split = blockIdx.x / npair;
+  const int lid = xcd_chunk(blockIdx.x, gridDim.x);
+  const int pair = lid % npair, split = lid / npair;
   const int cb = pair % n_co, kb = pair / n_co;
   const int c0 = cb * C::BCO, k0 = kb * C::BCI;
   const int t_begin = (int)((long long)split * n_tiles / splits);
@@ -80,55 +93,65 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(const dvie_wgrad_desc p
       (void*)((const char*)p.x + (size_t)k0 * 2), 0, (int)(xbytes - (unsigned long long)k0 * 2), 0x00020000);
   const unsigned grow = (unsigned)p.g_ld * 2u, xrow = (unsigned)p.x_ld * 2u;
 
-  // DMA lane geometry: piece q of a sub-image fills rows 8q .. 8q+7; lane -> row 8q + (lane>>3),
-  // LDS chunk (lane & 7) holding source chunk (lane & 7) ^ swz(row).  Channels past cout / c
-  // (padding of narrow layers) read as zeros.
+  // DMA lane geometry: a piece is 8 pixels x 128 B; lane -> pixel (lane>>3) of the piece and
+  // LDS chunk (lane & 7), holding source chunk (lane & 7) ^ swz(row).  Rows of 8 pixels start
+  // at multiples of 8, so swz(row) = 4 * ((row >> 1) & 1) depends on the lane only.
   const int lrow = lane >> 3, lch = lane & 7;
+  const int lcs = lch ^ (((lrow >> 1) & 1) << 2);
 
-  auto issue = [&](int tile, int buf) {
-    const int tx = tile % tiles_x;
-    const int t2 = tile / tiles_x;
-    const int ty = t2 % tiles_y, n = t2 / tiles_y;
-    const int y0 = ty * PR, x0 = tx * 64;
-    char* G = smem + buf * C::BUF;
-    char* X = G + C::GSZ;
+  struct TilePos {
+    int n, y0, x0, col;
+  };
+  auto tpos = [&](int t) {
+    TilePos q;
+    const int ty = t % tiles_y;
+    const int r = t / tiles_y;
+    q.x0 = (r % tiles_x) * 64;
+    q.n = r / tiles_x;
+    q.y0 = ty * PR;
+    q.col = r;
+    return q;
+  };
+
+  // G tile of tile T into G buffer gb
+  auto issue_g = [&](const TilePos& T, int gb) {
+    char* G = smem + gb * C::GSZ;
 #pragma unroll
-    for (int q = 0; q < C::GQ; ++q) {
-      const int pc = wave + 4 * q;  // piece over all sub-images
-      if (pc < C::NGP) {
+    for (int q = 0; q < (TMO * C::GPI + NW - 1) / NW; ++q) {
+      const int pc = wave + NW * q;
+      if (pc < TMO * C::GPI) {
         const int sub = pc / C::GPI, pr = pc - sub * C::GPI;
         const int row = pr * 8 + lrow;
-        const int oy = y0 + row / 64, ox = x0 + (row & 63);
-        const int cs = lch ^ (((row >> 1) & 1) << 2);
-        const int ch = 64 * sub + cs * 8;
+        const int oy = T.y0 + row / 64, ox = T.x0 + (row & 63);
+        const int ch = 64 * sub + lcs * 8;
         const unsigned o = (oy < p.oh && ox < p.ow && c0 + ch < p.cout)
-                               ? (unsigned)((n * p.oh + oy) * p.ow + ox) * grow + (unsigned)ch * 2u
+                               ? (unsigned)((T.n * p.oh + oy) * p.ow + ox) * grow + (unsigned)ch * 2u
                                : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_ptr_wg)(G + pc * 1024), 16, o, 0, 0, 0);
       }
     }
-#pragma unroll
-    for (int q = 0; q < C::XQ; ++q) {
-      const int pc = wave + 4 * q;
-      if (pc < C::NXP) {
-        const int sub = pc / C::XPI, pr = pc - sub * C::XPI;
-        const int row = pr * 8 + lrow;
-        const int hy = row / C::HWD, hx = row - (row / C::HWD) * C::HWD;
-        const int iy = y0 + p.dy0 + hy, ix = x0 + p.dx0 + hx;
-        const int cs = lch ^ (((row >> 1) & 1) << 2);
-        const int ch = 64 * sub + cs * 8;
-        const bool ok = row < C::XROWS && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw &&
-                        k0 + ch < p.c;
-        const unsigned o = ok ? (unsigned)((n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)ch * 2u : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_wg)(X + pc * 1024), 16, o, 0, 0, 0);
-      }
+  };
+  // halo rows [h0, h1) (relative to tile T's first halo row) into their ring slots
+  auto issue_x = [&](const TilePos& T, int h0, int h1) {
+    const int npc = (h1 - h0) * C::XPR;  // pieces per sub-image
+#pragma unroll 1
+    for (int pc = wave; pc < TMI * npc; pc += NW) {
+      const int sub = pc / npc, rem = pc - sub * npc;
+      const int hrow = h0 + rem / C::XPR, piece = rem - (rem / C::XPR) * C::XPR;
+      const int hx = piece * 8 + lrow;
+      const int iy = T.y0 + p.dy0 + hrow, ix = T.x0 + p.dx0 + hx;
+      const int slot = (T.y0 + hrow) % C::R;
+      const int ch = 64 * sub + lcs * 8;
+      const bool ok = hx < 64 + TW - 1 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw && k0 + ch < p.c;
+      const unsigned o = ok ? (unsigned)((T.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)ch * 2u : OOB;
+      char* dst = smem + 2 * C::GSZ + sub * C::XSUB + (slot * C::XW + piece * 8) * 128;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_wg)dst, 16, o, 0, 0, 0);
     }
   };
 
   // transposed-read lane addressing: lane 4q+p of 16-lane group grp reads row (4u + q) of the
   // group's 4-row block and 8 bytes at column 16*(grp&1) + 4p of the operand's 32 columns
   const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-  // byte offset inside a 64-channel sub-image for columns [col0, col0+32) and base row m (mod 4)
   auto tr_off = [&](int col0, int m) {
     const int row = m + tq;
     const int col = col0 + 16 * (grp & 1) + 4 * tp;
@@ -142,8 +165,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(const dvie_wgrad_desc p
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[a][e] = 0.f;
 
-  // waves 2 x 2 over (co, ci): wave owns 32*TMO co x 32*TMI ci
-  const int wco = wave >> 1, wci = wave & 1;
+  const int wco = (wave >> 1) & 1, wci = wave & 1, wrow = wave >> 2;
   int g_off[TMO], x_off[4][TMI];
 #pragma unroll
   for (int j = 0; j < TMO; ++j) {
@@ -159,48 +181,69 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(const dvie_wgrad_desc p
     }
 
   if (t_begin < t_end) {
-    issue(t_begin, 0);
+    const TilePos T0 = tpos(t_begin);
+    issue_g(T0, 0);
+    issue_x(T0, 0, C::HR);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
-  int buf = 0;
-  for (int tile = t_begin; tile < t_end; ++tile, buf ^= 1) {
-    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
-    const char* G = smem + buf * C::BUF;
-    const char* X = G + C::GSZ;
+  int gb = 0;
+  for (int tile = t_begin; tile < t_end; ++tile, gb ^= 1) {
+    const TilePos T = tpos(tile);
+    const bool has_next = tile + 1 < t_end;
+    const TilePos TN = tpos(has_next ? tile + 1 : tile);
+    const bool same_col = has_next && TN.col == T.col;
+    if (same_col) {  // next tile: its G tile and its PR new halo rows
+      issue_g(TN, gb ^ 1);
+      issue_x(TN, C::HR - PR, C::HR);
+    }
+    const char* G = smem + gb * C::GSZ;
+    const char* X = smem + 2 * C::GSZ;
 #pragma unroll
-    for (int py = 0; py < PR; ++py)
+    for (int pyl = 0; pyl < PR / 2; ++pyl)
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) {
+        const int py = wrow * (PR / 2) + pyl;
         const int gr = py * 64 + kx * 16;  // first G row of this k-step (multiple of 16)
         bf16x8 a[TMO];
 #pragma unroll
         for (int j = 0; j < TMO; ++j) a[j] = tr_pair(G + g_off[j] + gr * 128, G + g_off[j] + gr * 128 + 4 * 128);
 #pragma unroll
-        for (int t = 0; t < C::NT; ++t) {
-          const int ti = t / TW, tj = t % TW;
-          const int xr = (py + ti) * C::HWD + kx * 16 + tj;  // first X row (any alignment)
-          const int m = xr & 3, xb = xr - m;
+        for (int ti = 0; ti < TH; ++ti) {
+          const int slot = (T.y0 + py + ti) % C::R;  // ring slot of halo row py + ti (uniform)
+          const char* Xr = X + slot * (C::XW * 128);
 #pragma unroll
-          for (int ji = 0; ji < TMI; ++ji) {
-            const bf16x8 b = tr_pair(X + x_off[m][ji] + xb * 128, X + x_off[m][ji] + xb * 128 + 4 * 128);
+          for (int tj = 0; tj < TW; ++tj) {
+            const int t = ti * TW + tj;
+            const int xr = kx * 16 + tj;  // first pixel of the k-step in the halo row
+            const int m = xr & 3, xb = xr - m;
 #pragma unroll
-            for (int jo = 0; jo < TMO; ++jo) {
-              f32x16& c = acc[(t * TMO + jo) * TMI + ji];
-              c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[jo], b, c, 0, 0, 0);
+            for (int ji = 0; ji < TMI; ++ji) {
+              const bf16x8 b = tr_pair(Xr + x_off[m][ji] + xb * 128, Xr + x_off[m][ji] + xb * 128 + 4 * 128);
+#pragma unroll
+              for (int jo = 0; jo < TMO; ++jo) {
+                f32x16& c = acc[(t * TMO + jo) * TMI + ji];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[jo], b, c, 0, 0, 0);
+              }
             }
           }
         }
       }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    if (has_next && !same_col) {  // column change: refill the whole ring (pipeline restart)
+      issue_g(TN, gb ^ 1);
+      issue_x(TN, 0, C::HR);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
   }
 
   // ---- partial slab ws[split][co][t*c + ci] ----
   // C layout: column (ci) = lane & 31, rows (co) = 8*(e>>2) + 4*(lane>>5) + (e&3)
   const long long ws_k = (long long)C::NT * p.c;
   const int r32 = lane & 31, hh = lane >> 5;
-  float* slab = p.ws + (long long)split * p.cout * ws_k;
+  float* slab = p.ws + (long long)(2 * split + wrow) * p.cout * ws_k;
 #pragma unroll
   for (int t = 0; t < C::NT; ++t)
 #pragma unroll
@@ -233,7 +276,7 @@ struct WgPlan {
 };
 
 static WgPlan wgrad_plan(const dvie_wgrad_desc& p) {
-  if (p.th == 3) return {2, 1, 1};
+  if (p.th == 3) return {4, 1, 1};
   return {2, p.cout > 64 ? 2 : 1, p.c > 64 ? 2 : 1};
 }
 
@@ -252,12 +295,13 @@ int wgrad_halo_splits(const dvie_wgrad_desc& p) {
   const WgPlan w = wgrad_plan(p);
   int tx, ty, nt, nco, nci;
   wgrad_tiles(p, w, tx, ty, nt, nco, nci);
-  int s = (256 + nco * nci - 1) / (nco * nci);  // one workgroup per CU (LDS-bound), one wave of them
+  int s = 256 / (nco * nci);  // one workgroup per CU (LDS-bound): a single wave of workgroups
   if (s > nt) s = nt;
   return s < 1 ? 1 : s;
 }
 
-int wgrad_halo_slabs(const dvie_wgrad_desc& p) { return p.splits; }
+// two partial slabs per split (the two row halves of each workgroup)
+int wgrad_halo_slabs(const dvie_wgrad_desc& p) { return wgrad_halo_eligible(p) ? 2 * p.splits : p.splits; }
 
 bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   if (!wgrad_halo_eligible(p)) return false;
@@ -266,10 +310,10 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   wgrad_tiles(p, w, tiles_x, tiles_y, n_tiles, n_co, n_ci);
   const int grid = n_co * n_ci * p.splits;
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
-  hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits, \
+  hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
                      tiles_x, tiles_y, n_tiles)
   if (p.th == 3)
-    DVIE_WG(3, 2, 1, 1);
+    DVIE_WG(3, 4, 1, 1);
   else if (w.tmo == 2 && w.tmi == 2)
     DVIE_WG(1, 2, 2, 2);
   else if (w.tmo == 2)
