@@ -248,13 +248,16 @@ __global__ __launch_bounds__(256) void ssim_fwd_kernel(const dvie_loss_desc p) {
     const float s11 = e11 - m1 * m1, s22 = e22 - m2 * m2, s12 = e12 - m1 * m2;
     const float A = 2.f * m1 * m2 + C1, B = 2.f * s12 + C2;
     const float Cc = m1 * m1 + m2 * m2 + C1, D = s11 + s22 + C2;
-    const float S = (A * B) / (Cc * D);
+    const float Q = 1.f / (Cc * D);
+    const float S = (A * B) * Q;
     acc = S;
     if (p.grad) {
+      // derivatives written without dividing by A or B (either can cross zero: means of
+      // opposite sign, negative covariance), as autograd differentiates num / den
       const float inv = -1.f / ((float)p.bsz * p.ch * p.h * p.w);
-      const float dm1 = S * (2.f * m2 / A - 2.f * m2 / B - 2.f * m1 / Cc + 2.f * m1 / D);
+      const float dm1 = 2.f * Q * (m2 * (B - A) + m1 * S * (Cc - D));
       const float de11 = -S / D;
-      const float de12 = 2.f * S / B;
+      const float de12 = 2.f * A * Q;
       const long long plane_sz = (long long)p.h * p.w;
       const long long np = (long long)p.bsz * p.ch * plane_sz;
       const long long idx = (long long)plane * plane_sz + (long long)oy * p.w + ox;

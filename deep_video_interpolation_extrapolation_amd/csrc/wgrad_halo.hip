@@ -18,6 +18,8 @@
 // partial slabs.  The slabs are summed by dvie_wgrad_reduce.
 //
 // Reference op replaced: nn.Conv2d backward-weight (nets/HRNet.py, nets/vgg.py).
+#include <stdlib.h>
+
 #include "common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -262,6 +264,8 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
 
 static bool wgrad_halo_eligible(const dvie_wgrad_desc& p) {
   if (p.dtype != DVIE_BF16) return false;
+  const char* e = getenv("DVIE_WGRAD_HALO");  // diagnostic override: 0 = per-tap kernel only
+  if (e && *e == '0') return false;
   if (p.sy != 1 || p.sx != 1 || p.ddy != 1 || p.ddx != 1) return false;
   if (!((p.th == 1 && p.tw == 1) || (p.th == 3 && p.tw == 3))) return false;
   if (p.c % 8 != 0 || p.cout % 8 != 0) return false;

@@ -20,6 +20,7 @@ kernels never allocate.  Reference semantics: nets/HRNet.py, nets/vgg.py, losses
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -27,6 +28,7 @@ from . import _lib as L
 
 PADC = 8  # channel padding granule (16-byte bf16 vectors)
 PROFILE = None  # set to a list to time every op with HIP events (bench profiling steps)
+DEBUG_NAN = bool(os.environ.get("DVIE_DEBUG_NAN"))  # op-by-op non-finite tracing (diagnostics only)
 
 
 def rup(x, m):
@@ -797,10 +799,30 @@ class Plan:
             if first:
                 d.beta = int(accumulate)
 
+    def _nonfinite(self):
+        """names of buffers (activations / gradients) holding non-finite values (debug)."""
+        out = set()
+        for b in self.g.buffers:
+            for tag, t in (("A", b.t), ("G", b.g)):
+                if t is not None and t.is_floating_point() and not bool(torch.isfinite(t).all()):
+                    out.add(f"{tag}:{b.name}")
+        return out
+
     def _run(self, arr, start, end, s, what, metas):
         lib = L.load()
         base = ctypes.addressof(arr)
         sz = ctypes.sizeof(L.Op)
+        if DEBUG_NAN:  # op-by-op, report the first op after which new buffers turn non-finite
+            seen = self._nonfinite()
+            for i in range(start, end):
+                L.check(lib.dvie_run_ops(base + i * sz, 1, s), what)
+                torch.cuda.synchronize()
+                now = self._nonfinite()
+                if now - seen:
+                    print(f"[dvie nan] {what} op {i} kind {arr[i].kind} meta {metas[i] if metas else None}: "
+                          f"{sorted(now - seen)}", flush=True)
+                    seen = now
+            return
         if PROFILE is None:
             L.check(lib.dvie_run_ops(base + start * sz, end - start, s), what)
             return

@@ -472,6 +472,9 @@ class HRNet(FlatParams, nn.Module):
         accumulate = self.grad_views()
         plan.set_param_grads(accumulate)
         g_rgb, g_seg = grads
+        if E.DEBUG_NAN:
+            print(f"[dvie nan] HRNet output grads finite: rgb {bool(torch.isfinite(g_rgb).all())} "
+                  f"seg {bool(torch.isfinite(g_seg).all())}", flush=True)
         plan.set_output_grad("rgb", g_rgb.float())
         plan.set_output_grad("segout", g_seg.float())
         hook = self.grad_hook

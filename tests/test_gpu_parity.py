@@ -89,6 +89,20 @@ def test_pixel_losses(dev, name):
     assert abs(v2 - vr) <= 1e-5 * max(1, abs(vr)) and rel_err(g2, gr) < 1e-4
 
 
+def test_ssim_gradient_near_degenerate(dev):
+    """Prediction ~ small negative constant, target positive: the SSIM terms
+    2*mu1*mu2 + C1 and 2*sigma12 + C2 cross zero at some pixels; the gradient must stay finite
+    and match autograd of the reference formula (losses.py:18-48)."""
+    from deep_video_interpolation_extrapolation_amd import losses as DL
+    torch.manual_seed(7)
+    gt = torch.rand(2, 3, 48, 64)
+    pred = -0.02 + 0.003 * torch.randn(2, 3, 48, 64)
+    v, vr, g, gr = _loss_pair(dev, DL.ssim_loss, OL.ssim_loss, pred, gt)
+    assert torch.isfinite(g).all() and torch.isfinite(gr).all()
+    assert abs(v - vr) <= 1e-5 * max(1, abs(vr))
+    assert rel_err(g, gr) < 1e-3
+
+
 def test_cross_entropy(dev):
     from deep_video_interpolation_extrapolation_amd import losses as DL
     logits, onehot = inputs.ce_inputs()
