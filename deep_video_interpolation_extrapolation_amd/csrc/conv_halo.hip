@@ -504,6 +504,242 @@ static int env_cfg() {
   return e && *e ? atoi(e) : -3;
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight-stationary variant for single-chunk 3x3 convs (c <= 64, cout <= 64: the 64-channel
+// full-resolution HRNet branch, its data gradient, VGG conv1_2): every wave keeps the
+// weights of its 32 output channels for all 9 taps in VGPRs (loaded once per workgroup), so
+// the tap loop reads only input-halo fragments from LDS and needs no barrier; one barrier
+// per output tile (halo double buffer).  8 waves = 2 channel halves x 4 output rows.
+template <int KS, bool OUTF32>
+__global__ __launch_bounds__(512) void conv_ws_kernel(const dvie_conv_desc p, int n_tiles, int tiles_x, int tiles_y,
+                                                      int persistent) {
+  typedef HaloCfg<1, 2, 4, 3, 3> C;  // halo geometry of a 4-row x 64-pixel tile, 8 waves
+  constexpr int NW = 8;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * C::HSZ];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave >> 2, wp = wave & 3;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  int tile0, tile_end, tile_step;
+  if (!persistent) {
+    tile0 = xcd_remap3(blockIdx.x, n_tiles);
+    tile_end = tile0 + 1;
+    tile_step = 1;
+  } else {
+    const int G = gridDim.x, g = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int nbg = G / 8 + (g < G % 8 ? 1 : 0);
+    const int q = n_tiles / 8, r = n_tiles % 8;
+    const int ts = g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q;
+    tile0 = ts + j;
+    tile_end = ts + q + (g < r ? 1 : 0);
+    tile_step = nbg;
+  }
+  if (tile0 >= tile_end) return;
+
+  // ---- weights -> VGPRs: lane (r32, h) holds w[co][t*c + 16s + 8h .. +7], co = 32*wc + r32
+  i32x4 wa[9][KS];
+  {
+    const int co = 32 * wc + r32;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int sl = 0; sl < KS; ++sl) {
+        const int k = 16 * sl + 8 * hh;
+        i32x4 v = {0, 0, 0, 0};
+        if (co < p.cout && k < p.c) v = *(const i32x4*)((const bf16_t*)p.w + (long long)co * p.kpad + t * p.c + k);
+        wa[t][sl] = v;
+      }
+  }
+
+  int hgeo[C::NHQ];
+#pragma unroll
+  for (int q = 0; q < C::NHQ; ++q) {
+    const int slot = (wave + NW * q) * 64 + lane;
+    const int hr = slot / 9, cs = slot - 9 * (slot / 9);
+    const int hy = hr / C::HWD, hx = hr - (hr / C::HWD) * C::HWD;
+    hgeo[q] = (cs < 8 && cs * 8 < p.c && hr < C::HR * C::HWD) ? (hy << 16) | (hx << 4) | cs : -1;
+  }
+  const unsigned xrow = (unsigned)p.x_ld * 2u;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)xbytes, 0x00020000);
+
+  struct TP {
+    int n, y0, x0;
+  };
+  auto decode = [&](int t) {
+    TP q;
+    q.x0 = (t % tiles_x) * 64;
+    const int r = t / tiles_x;
+    q.y0 = (r % tiles_y) * C::PR;
+    q.n = r / tiles_y;
+    return q;
+  };
+  auto halo_issue = [&](const TP& T, int hb) {
+    char* dst = smem + hb * C::HSZ + wave * 1024;
+    const int ybase = T.y0 + p.dy0, xbase = T.x0 + p.dx0;
+#pragma unroll
+    for (int q = 0; q < C::NHQ; ++q) {
+      const int gq = hgeo[q];
+      const int iy = ybase + (gq >> 16), ix = xbase + ((gq >> 4) & 0xFFF);
+      const bool ok = gq >= 0 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw;
+      const unsigned o = ok ? (unsigned)((T.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)(gq & 15) * 16u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(dst + q * NW * 1024), 16, o, 0, 0, 0);
+    }
+  };
+
+  const int b_base = (wp * C::HWD + r32) * C::PITCH + hh * 16;
+  TP cur = decode(tile0);
+  halo_issue(cur, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  int hb = 0;
+  for (int tile = tile0; tile < tile_end; tile += tile_step, hb ^= 1) {
+    const bool has_next = tile + tile_step < tile_end;
+    const TP nxt = decode(has_next ? tile + tile_step : tile);
+    if (has_next) halo_issue(nxt, hb ^ 1);
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+    const char* H = smem + hb * C::HSZ + b_base;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ti = t / 3, tj = t % 3;
+#pragma unroll
+      for (int sl = 0; sl < KS; ++sl) {
+        i32x4 bf[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[b] = *(const i32x4*)(H + (ti * C::HWD + 32 * b + tj) * C::PITCH + sl * 32);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa[t][sl]),
+                                                           __builtin_bit_cast(bf16x8, bf[b]), acc[b], 0, 0, 0);
+      }
+    }
+    // the next tile's halo has landed and every wave is done with this one
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- epilogue straight from the accumulators (as conv_halo_kernel) ----
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float v[2][8];
+#pragma unroll
+      for (int P = 0; P < 2; ++P)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[b][8 * P + e]),
+                                                           __float_as_uint(acc[b][8 * P + 4 + e]), false, false);
+          v[P][e] = __uint_as_float(sw[0]);
+          v[P][4 + e] = __uint_as_float(sw[1]);
+        }
+      const int oy = cur.y0 + wp, ox = cur.x0 + 32 * b + r32;
+      if (oy >= p.oh || ox >= p.ow) continue;
+      const long long pix = ((long long)cur.n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        const int co = 32 * wc + 16 * P + 8 * hh;
+        if (co >= p.cout) continue;
+        float* w = v[P];
+        if (p.bias) {
+          const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            w[e] += b0[e];
+            w[4 + e] += b1[e];
+          }
+        }
+        float t8[8];
+        if constexpr (OUTF32) {
+          float* dst = (float*)p.y + pix * p.y_ld + co;
+          if (p.res) {
+            const float* rs = (const float*)p.res + pix * p.res_ld + co;
+            const f32x4 r0 = *(const f32x4*)rs, r1 = *(const f32x4*)(rs + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[e] += r0[e];
+              w[4 + e] += r1[e];
+            }
+          }
+          if (p.beta) {
+            const f32x4 r0 = *(const f32x4*)dst, r1 = *(const f32x4*)(dst + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[e] += r0[e];
+              w[4 + e] += r1[e];
+            }
+          }
+          act_apply(w, 8, p.act, p.alpha);
+          if (p.dact) {
+            const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              t8[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
+              t8[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
+            }
+            dact_apply(w, t8, 8, p.dact, p.alpha);
+          }
+          *(f32x4*)dst = f32x4{w[0], w[1], w[2], w[3]};
+          *(f32x4*)(dst + 4) = f32x4{w[4], w[5], w[6], w[7]};
+        } else {
+          bf16_t* dst = (bf16_t*)p.y + pix * p.y_ld + co;
+          if (p.res) {
+            const i32x4 tr = *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+              w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+            }
+          }
+          if (p.beta) {
+            const i32x4 tr = *(const i32x4*)dst;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+              w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+            }
+          }
+          act_apply(w, 8, p.act, p.alpha);
+          if (p.dact) {
+            const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              t8[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
+              t8[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
+            }
+            dact_apply(w, t8, 8, p.dact, p.alpha);
+          }
+          i32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
+          *(i32x4*)dst = o;
+        }
+      }
+    }
+    cur = nxt;
+  }
+}
+
+template <int KS>
+static void launch_ws(const dvie_conv_desc& p, hipStream_t s) {
+  const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + 3) / 4;
+  const int n_tiles = tiles_x * tiles_y * p.n;
+  const int persistent = n_tiles > 256 ? 1 : 0;
+  const int grid = persistent ? 256 : n_tiles;
+  if (p.out_f32)
+    hipLaunchKernelGGL((conv_ws_kernel<KS, true>), dim3(grid), dim3(512), 0, s, p, n_tiles, tiles_x, tiles_y,
+                       persistent);
+  else
+    hipLaunchKernelGGL((conv_ws_kernel<KS, false>), dim3(grid), dim3(512), 0, s, p, n_tiles, tiles_x, tiles_y,
+                       persistent);
+}
+
 // Returns true when the halo kernel took the launch.
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (p.dtype != DVIE_BF16) return false;
@@ -517,6 +753,16 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (pix >= (1ull << 31)) return false;
   int cfg = env_cfg();
   if (cfg == -1) return false;
+  if (t3 && p.c <= 64 && p.cout <= 64 && (cfg == -3 || cfg == 8) && (long long)p.n * p.oh * p.ow >= 65536) {
+    // single input chunk, one 64-channel output tile: weights stay in VGPRs
+    switch ((p.c + 15) / 16) {
+      case 1: launch_ws<1>(p, s); break;
+      case 2: launch_ws<2>(p, s); break;
+      case 3: launch_ws<3>(p, s); break;
+      default: launch_ws<4>(p, s); break;
+    }
+    return true;
+  }
   if (cfg < 0) {  // measured on MI355X (tools/conv_tune.py): see DESIGN.md
     if (p.cout <= 32)
       cfg = 2;
