@@ -255,7 +255,7 @@ class HRNet(FlatParams, nn.Module):
         cm += list(range(3 * F)) + [-1] * (E.rup(3 * F, 8) - 3 * F)
         return cm
 
-    def _lower(self, g, H, W, dry=False):
+    def _lower(self, g, H, W, dry=False, xgrad=False):
         A = L
         rup = E.rup
         F = self.n_frames
@@ -270,7 +270,8 @@ class HRNet(FlatParams, nn.Module):
             e2 = g.buffer(f"seg{k}_e2", H, W, 32)
             g.conv(E.R(e1), self.seg_encoder[2], E.R(e2), act=A.ACT_ELU, name="seg_encoder.2")
             g.conv(E.R(e2), self.seg_encoder[4], E.R(feat, 8 * k, 8), name="seg_encoder.4")
-        g.input_nchw(E.R(feat, 8 * F, rup(3 * F, 8)), "x", ext_c=3 * F)
+        # xgrad: the frames input needs a gradient (ExtraTrainer rollout feeds a prediction back)
+        g.input_nchw(E.R(feat, 8 * F, rup(3 * F, 8)), "x", ext_c=3 * F, requires_grad=xgrad)
         s1 = g.buffer("stem1", H, W, 64)
         g.conv(E.R(feat), self.conv1, E.R(s1), act=A.ACT_LRELU, cmap=self._stem_cmap(), name="conv1")
         s2 = g.buffer("stem2", H, W, 64)
@@ -420,8 +421,8 @@ class HRNet(FlatParams, nn.Module):
         g.output("segout", E.R(seg), self.seg_out_dim)
 
     def _build_plan(self, key):
-        n, H, W, dtype, train, dev = key
-        g = self._lower(E.Graph(dtype), H, W)
+        n, H, W, dtype, train, dev, xgrad = key
+        g = self._lower(E.Graph(dtype), H, W, xgrad=xgrad)
         return g.compile(n, dev, backward=train)
 
     def _on_moved(self):
@@ -432,7 +433,8 @@ class HRNet(FlatParams, nn.Module):
         x, seg = inputs
         n, _, H, W = x.shape
         L.require_gpu(x)
-        plan = self._pool.acquire((n, H, W, self.dtype, bool(train), x.device))
+        xgrad = bool(train) and bool(getattr(self, "_in_needs", (False,))[0])
+        plan = self._pool.acquire((n, H, W, self.dtype, bool(train), x.device, xgrad))
         plan.set_input("x", x)
         plan.set_input("seg", seg)
         rgb = torch.empty((n, H, W, E.rup(self.rgb_out_dim, 8)), dtype=torch.float32, device=x.device)
@@ -477,6 +479,10 @@ class HRNet(FlatParams, nn.Module):
                   f"seg {bool(torch.isfinite(g_seg).all())}", flush=True)
         plan.set_output_grad("rgb", g_rgb.float())
         plan.set_output_grad("segout", g_seg.float())
+        gx = None
+        if "x" in plan.ext_grad:
+            gx = torch.empty(inputs[0].shape, dtype=torch.float32, device=inputs[0].device)
+            plan.set_input_grad("x", gx)
         hook = self.grad_hook
         if hook is None:
             plan.run_backward()
@@ -484,7 +490,7 @@ class HRNet(FlatParams, nn.Module):
             cuts, ranges = self._buckets(plan, hook[0])
             plan.run_backward(cuts=cuts, on_cut=lambda k: hook[1](*ranges[k]))
             hook[1](*ranges[-1])
-        return [None, None]
+        return [gx, None]
 
     def forward_split(self, x, seg):
         """x: (B, 3F, H, W) frames in [-1, 1]; seg: (B, 20F, H, W) one-hot segmentations."""

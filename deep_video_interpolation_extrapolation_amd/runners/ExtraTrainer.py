@@ -1,0 +1,182 @@
+"""ExtraTrainer on the MI355X path (reference runners/ExtraTrainer.py).
+
+Extrapolation: frames 1, 2 (and their segmentations) -> frame 3 (and, with
+`--num_pred_once k`, frames 3..2+k from one forward).  Same hot path as InterTrainer
+(HRNet plan, RGBLoss + CE kernels, plan backward with in-backward RCCL buckets, fused
+Adamax); the step body is the reference's l.234-323 factored into `step(data)`.
+
+Loss keys follow the reference: `step_{i}_frame_{j}_coarse_{l1,gdl,vgg,ssim,ce}_loss`
+and `loss_all` (l.286-315).
+
+Reference defects this build does not reproduce:
+  * l.65 `RGBLoss(args, sharp=False)` raises TypeError (RGBLoss has no `sharp`), so the
+    reference train split cannot start; here RGBLoss(args) is constructed.
+  * l.304-310 (rollout, `num_pred_step > 1`) reads the undefined `out_img` /
+    `inpainted_img` / `out_seg`.  Here the rollout uses this step's prediction as the
+    intended value: next input = [x[:, -3:], coarse_img] / [seg[:, -20:],
+    onehot(argmax(coarse_seg))], gradients flowing back through coarse_img into the
+    previous step (as the reference graph would, had it run).
+  * l.188 `d[...]:0` (annotation, not assignment) only affects rank-0 logging.
+The inpainting branch (`--inpaint`, InpaintUnet) has no model definition anywhere in the
+reference tree and raises NotImplementedError here.
+"""
+from collections import OrderedDict
+
+import torch
+
+from .. import _lib as L
+from ..data import batch_to
+from . import comm
+from .InterTrainer import InterTrainer
+
+
+def onehot_argmax(seg, n_classes=20):
+    """torch.eye(20)[seg.argmax(1)].permute(0,3,1,2) (reference l.310), on device."""
+    lab = seg.argmax(dim=1)
+    return torch.nn.functional.one_hot(lab, n_classes).permute(0, 3, 1, 2).float().contiguous()
+
+
+class ExtraTrainer(InterTrainer):
+    def __init__(self, args):
+        if getattr(args, "inpaint", False):
+            raise NotImplementedError("--inpaint: InpaintUnet is not defined in the reference tree")
+        args.syn_type = "extra"
+        super().__init__(args)
+
+    def get_input(self, data):
+        """reference l.109-114"""
+        x = torch.cat([data["frame1"], data["frame2"]], dim=1)
+        seg = torch.cat([data["seg1"], data["seg2"]], dim=1) if self.args.mode == "xs2xs" else None
+        vl = getattr(self.args, "vid_length", 1)
+        gt_x = [data["frame" + str(i + 3)] for i in range(vl)]
+        gt_seg = [data["seg" + str(i + 3)] if self.args.mode == "xs2xs" else None for i in range(vl)]
+        return x, seg, gt_x, gt_seg
+
+    def step(self, data):
+        """One training step (reference l.249-323)."""
+        a = self.args
+        npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
+        if nps > 1:
+            assert npo == 1, "rollout (num_pred_step > 1) requires num_pred_once == 1 (reference l.252-253)"
+        data = batch_to(data, self.device)
+        xs2xs = a.mode == "xs2xs"
+        loss_dict = OrderedDict()
+        last_rgb = torch.cat([data["frame1"], data["frame2"]], dim=1)
+        last_seg = torch.cat([data["seg1"], data["seg2"]], dim=1) if xs2xs else None
+        for ii in range(nps):
+            g0 = 3 + ii * npo
+            gt_x = torch.cat([data["frame" + str(i)] for i in range(g0, g0 + npo)], dim=1)
+            gt_seg = torch.cat([data["seg" + str(i)] for i in range(g0, g0 + npo)], dim=1) if xs2xs else None
+            x, seg = last_rgb, last_seg
+            if getattr(a, "fix_init_frames", False):
+                x = torch.cat([data["frame2"], x], dim=1)
+                if xs2xs:
+                    seg = torch.cat([data["seg2"], seg], dim=1)
+            out = self.model(x, seg=seg, gt_x=gt_x, gt_seg=gt_seg)
+            coarse_img, coarse_seg = out[0], out[1]
+            for j in range(npo):
+                prefix = "step_{}_frame_{}_coarse".format(ii + 1, j + 1)
+                loss_dict.update(self.RGBLoss(coarse_img[:, 3 * j:3 * j + 3], gt_x[:, 3 * j:3 * j + 3], False,
+                                              prefix=prefix))
+                if xs2xs:
+                    loss_dict[prefix + "_ce_loss"] = a.ce_weight * self.SegLoss(
+                        coarse_seg[:, 20 * j:20 * j + 20], gt_seg[:, 20 * j:20 * j + 20])
+            if nps == 1:
+                break
+            last_rgb = torch.cat([x[:, -3:], coarse_img], dim=1)
+            if xs2xs:
+                last_seg = torch.cat([seg[:, -20:], onehot_argmax(coarse_seg)], dim=1)
+        loss = 0
+        for v in loss_dict.values():
+            loss = loss + torch.mean(v)
+        loss_dict["loss_all"] = loss
+        self.coarse_opt.zero_grad(set_to_none=True)
+        (loss / self.W).backward()  # reference `sync` divides loss_all by W in place (l.317, 760-765)
+        self.model.finish()
+        if getattr(a, "train_coarse", False):
+            self.coarse_opt.step()
+        self.global_step += 1
+        return comm.sync_losses(OrderedDict((k, v.detach()) for k, v in loss_dict.items()), self.W)
+
+    def validate(self):
+        """Reference l.421-583: per (step, frame) L1 / PSNR / SSIM / IoU / VGG-cos."""
+        a = self.args
+        self.log.info("Validation epoch {} started".format(self.epoch))
+        self.model.eval()
+        npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
+        crit = ["coarse_l1", "coarse_psnr", "coarse_ssim", "coarse_vgg", "coarse_iou"]
+        from ..utils.net_utils import AverageMeter
+        meters = OrderedDict()
+        with torch.no_grad():
+            for data in self.val_loader:
+                data = batch_to(data, self.device)
+                last_rgb = torch.cat([data["frame1"], data["frame2"]], dim=1)
+                last_seg = torch.cat([data["seg1"], data["seg2"]], dim=1)
+                d = OrderedDict()
+                for i in range(nps):
+                    g0 = 3 + i * npo
+                    gt_x = torch.cat([data["frame" + str(k)] for k in range(g0, g0 + npo)], dim=1)
+                    gt_seg = torch.cat([data["seg" + str(k)] for k in range(g0, g0 + npo)], dim=1)
+                    x, seg = last_rgb, last_seg
+                    if getattr(a, "fix_init_frames", False):
+                        x = torch.cat([data["frame2"], x], dim=1)
+                        seg = torch.cat([data["seg2"], seg], dim=1)
+                    out = self.model(x, seg=seg, gt_x=gt_x, gt_seg=gt_seg)
+                    coarse_img, coarse_seg = out[0], out[1]
+                    for j in range(npo):
+                        p = "step_{}_frame_{}_".format(i, j)
+                        im = self.normalize(coarse_img[:, 3 * j:3 * j + 3])
+                        gt = self.normalize(gt_x[:, 3 * j:3 * j + 3])
+                        d[p + "coarse_l1"] = self.L1Loss(im, gt)
+                        d[p + "coarse_psnr"] = self.PSNRLoss(im, gt)
+                        d[p + "coarse_ssim"] = 1 - self.SSIMLoss(im, gt)
+                        d[p + "coarse_iou"] = self.IoULoss(torch.argmax(coarse_seg[:, 20 * j:20 * j + 20], dim=1),
+                                                           torch.argmax(gt_seg[:, 20 * j:20 * j + 20], dim=1))
+                        d[p + "coarse_vgg"] = self.VGGCosLoss(im, gt, False)
+                    if nps == 1:
+                        break
+                    last_rgb = torch.cat([x[:, -3:], coarse_img], dim=1)
+                    last_seg = torch.cat([seg[:, -20:], onehot_argmax(coarse_seg)], dim=1)
+                d = comm.sync_losses(d, self.W)
+                if self.rank == 0:
+                    for k, v in d.items():
+                        meters.setdefault(k, AverageMeter()).update(float(v), data["frame1"].size(0) * self.W)
+        res = OrderedDict((k, m.avg) for k, m in meters.items())
+        if self.rank == 0:
+            self.log.info("Epoch [{}] Evaluation: ".format(self.epoch) + " ".join(f"{k} [{v:.3f}]" for k, v in res.items()))
+            self._scalars("val/score", res)
+        return res
+
+    def mini_test(self, img_list, seg_list):
+        """Reference l.681-757: autoregressive rollout from two [0,1] frames (and one-hot or
+        label segmentations).  Returns per-step predicted images in [0,1] and label maps."""
+        assert len(img_list) == 2 and len(seg_list) == 2
+        if seg_list[0].dim() == 3:
+            seg_list = [torch.nn.functional.one_hot(s.long(), 20).permute(0, 3, 1, 2).float() for s in seg_list]
+        self.model.eval()
+        dev = self.device
+        a = self.args
+        npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
+        pred_img, pred_seg = [], []
+        with torch.no_grad():
+            i1, i2 = img_list[0].to(dev) * 2 - 1, img_list[1].to(dev) * 2 - 1
+            s1, s2 = seg_list[0].to(dev), seg_list[1].to(dev)
+            for _ in range(nps):
+                img, seg = self.model(torch.cat([i1, i2], 1), torch.cat([s1, s2], 1))[:2]
+                for j in range(npo):
+                    pred_img.append(self.normalize(img[:, 3 * j:3 * j + 3]))
+                    pred_seg.append(torch.argmax(seg[:, 20 * j:20 * j + 20], dim=1))
+                if npo == 1:
+                    i1, i2 = i2, pred_img[-1] * 2 - 1
+                    s1, s2 = s2, onehot_argmax(seg[:, :20])
+                else:
+                    i1, i2 = pred_img[-2] * 2 - 1, pred_img[-1] * 2 - 1
+                    s1 = torch.nn.functional.one_hot(pred_seg[-2], 20).permute(0, 3, 1, 2).float()
+                    s2 = torch.nn.functional.one_hot(pred_seg[-1], 20).permute(0, 3, 1, 2).float()
+        return [p.cpu() for p in pred_img], [s.cpu() for s in pred_seg]
+
+    def save_checkpoint(self):
+        return super().save_checkpoint()
+
+
+__all__ = ["ExtraTrainer", "onehot_argmax", "L"]

@@ -53,17 +53,22 @@ class GradSync:
     def __getattr__(self, name):
         return getattr(self.__dict__["module"], name)
 
-    def finish(self):
-        """Wait for the bucket all-reduces (stream-ordered) and apply the 1/W factor."""
-        if self.W == 1:
-            return
+    def wait(self):
+        """Join the bucket all-reduces (stream-ordered on the GPU)."""
         for w in self.works:
             w.wait()
         self.works = []
+
+    def finish(self):
+        """Wait for the bucket all-reduces and apply the 1/W factor (HIP kernel)."""
+        if self.W == 1:
+            return
+        self.wait()
         lib = L.load()
         for m in self.flat_owners:
             g = m._flat_grad
             if g is not None:
+                L.require_gpu(g)
                 L.check(lib.dvie_scale(g.data_ptr(), g.numel(), 1.0 / self.W, L.stream_ptr(g.device)), "grad scale")
 
     def train(self, mode=True):

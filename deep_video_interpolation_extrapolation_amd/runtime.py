@@ -139,6 +139,7 @@ class PlanFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, runner, n_in, *args):
         inputs = args[:n_in]
+        runner._in_needs = tuple(ctx.needs_input_grad[2:2 + n_in])  # which inputs want a gradient
         plan, outs = runner.run_forward(inputs, any(ctx.needs_input_grad))
         ctx.runner = runner
         ctx.token = _Token(plan) if plan is not None and plan.backward_enabled else None

@@ -60,3 +60,18 @@ def adamax(params, grads, lr, state=None, betas=(0.9, 0.999), eps=1e-8):
         clr = lr / (1 - betas[0] ** s["step"])
         new[k] = p - clr * (s["exp_avg"] / s["exp_inf"])
     return new, state
+
+
+def extra_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(80.0, 80.0, 20.0, 20.0, 30.0)):
+    """One ExtraTrainer step, num_pred_once = num_pred_step = 1 (reference
+    runners/ExtraTrainer.py:249-323): x = cat(frame1, frame2), seg = cat(seg1, seg2),
+    target frame3 / seg3; loss keys 'step_1_frame_1_coarse_*'.  With one predicted frame
+    the extrapolation HRNet has the interpolation HRNet's shapes (nets/HRNet.py:351-356),
+    so the step is inter_step on the remapped sample."""
+    remap = {"frame1": data["frame1"], "frame3": data["frame2"], "frame2": data["frame3"],
+             "seg1": data["seg1"], "seg3": data["seg2"], "seg2": data["seg3"]}
+    ld, grads, new, state, outs = inter_step(params, vgg_state, remap, lr, world, state, weights)
+    ren = OrderedDict()
+    for k, v in ld.items():
+        ren["step_1_frame_1_" + k if k.startswith("coarse") else k] = v
+    return ren, grads, new, state, outs

@@ -1,0 +1,85 @@
+"""GPU: ExtraTrainer (reference runners/ExtraTrainer.py) on the HIP path.
+
+* one fp32 step against the CPU oracle's extra_step (same HRNet / RGBLoss / CE / Adamax
+  math; the reference's own ExtraTrainer cannot be constructed, SURVEY §0.4, so parity is
+  anchored on the oracle, itself pinned by the reference InterTrainer step fixture);
+* the HRNet frames-input gradient that the autoregressive rollout needs, against
+  torch.autograd through the oracle HRNet (fp32, 1e-4 relative);
+* rollout (num_pred_step 2) and multi-frame (num_pred_once 2) steps train in bf16.
+"""
+import numpy as np
+import pytest
+import torch
+
+import inputs
+from oracle import hrnet as O
+from oracle import losses as OL
+from oracle import step as OS
+
+pytestmark = pytest.mark.gpu
+
+
+def extra_trainer(prec, H, W, B, **kw):
+    import os
+    from deep_video_interpolation_extrapolation_amd.options import default_args
+    from deep_video_interpolation_extrapolation_amd.runners.ExtraTrainer import ExtraTrainer
+    args = default_args("EXTRA", syn_type="extra", train_coarse=True, batch_size=B, input_h=H, input_w=W,
+                        precision=prec, synthetic=B, num_workers=0, split="train", **kw)
+    os.environ["DVIE_PRECISION"] = prec
+    torch.manual_seed(1024)
+    return ExtraTrainer(args)
+
+
+def test_extra_step_matches_oracle(dev):
+    """loss dict within 1e-4 relative; post-Adamax weight checksums within 1e-4 relative
+    (see test_gpu_train for why checksums rather than max-abs)."""
+    tr = extra_trainer("fp32", 32, 64, 2)
+    data = inputs.step_batch(2, 32, 64)
+    ld = tr.step(data)
+    P = O.init_params(1024)
+    ref, grads, new, _, _ = OS.extra_step(P, OL.synthetic_vgg19_state(), data)
+    assert list(ld.keys()) == list(ref.keys())
+    np.testing.assert_allclose([float(ld[k]) for k in ref], [ref[k] for k in ref], rtol=1e-4)
+    named = dict(tr.model.module.coarse_model.named_parameters())
+    post = np.array([float((named[n].detach().double() ** 2).sum()) for n in new])
+    want = np.array([float((new[n].double() ** 2).sum()) for n in new])
+    np.testing.assert_allclose(post, want, rtol=1e-4)
+
+
+def test_hrnet_frames_input_gradient(dev, monkeypatch):
+    """d/dx of <rgb, R1> + <seg, R2> through the HIP plan vs the oracle's autograd."""
+    monkeypatch.setenv("DVIE_PRECISION", "fp32")
+    import types
+    from deep_video_interpolation_extrapolation_amd import nets
+    torch.manual_seed(1024)
+    m = nets.InterNet(types.SimpleNamespace(syn_type="inter", highres_large=False, coarse_model="HRNet")).to(dev)
+    x, seg = inputs.hrnet_input(2, 16, 32)
+    g = torch.Generator().manual_seed(5)
+    r1 = torch.randn((2, 3, 16, 32), generator=g)
+    r2 = torch.randn((2, 20, 16, 32), generator=g)
+    xd = x.to(dev).requires_grad_(True)
+    rgb, s = m(xd, seg.to(dev))
+    ((rgb * r1.to(dev)).sum() + (s * r2.to(dev)).sum()).backward()
+    torch.cuda.synchronize()
+    P = O.init_params(1024)
+    xr = x.clone().requires_grad_(True)
+    rr, sr = O.forward(P, torch.cat([xr, seg], 1))
+    ((rr * r1).sum() + (sr * r2).sum()).backward()
+    err = float((xd.grad.cpu() - xr.grad).abs().max() / xr.grad.abs().max())
+    assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("kw", [dict(num_pred_step=2), dict(num_pred_once=2, vid_length=2)])
+def test_extra_bf16_variants_train(dev, kw):
+    from deep_video_interpolation_extrapolation_amd.data import SyntheticClips
+    tr = extra_trainer("bf16", 64, 128, 2, **kw)
+    k = 2 + max(kw.get("vid_length", 1), kw.get("num_pred_step", 1))
+    ds = SyntheticClips(2, 64, 128, k)
+    items = [ds[i] for i in range(2)]
+    data = {key: torch.stack([it[key] for it in items]) for key in items[0]}
+    losses = [float(tr.step(data)["loss_all"]) for _ in range(5)]
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < losses[0], losses
+    keys = list(tr.step(data).keys())
+    n = kw.get("num_pred_step", 1) * kw.get("num_pred_once", 1)
+    assert sum(k.endswith("_ce_loss") for k in keys) == n
