@@ -20,6 +20,7 @@ ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU = 0, 1, 2, 3
 EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW = range(8)
 LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC = range(6)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
+OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD = 8, 9, 10, 11
 
 vp = ctypes.c_void_p
 i32 = ctypes.c_int
@@ -113,6 +114,35 @@ class WarpDesc(ctypes.Structure):
     ]
 
 
+class BnDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", vp), ("y", vp), ("g", vp), ("dx", vp), ("gamma", vp), ("beta", vp), ("dgamma", vp), ("dbeta", vp),
+        ("running_mean", vp), ("running_var", vp), ("partial", vp), ("stats", vp),
+        ("x_ld", i64), ("y_ld", i64), ("g_ld", i64), ("dx_ld", i64), ("rows", i64),
+        ("c", i32), ("splits", i32), ("act", i32), ("training", i32),
+        ("dtype", i32), ("accumulate", i32), ("beta_dx", i32), ("pad0", i32),
+        ("alpha", f32), ("eps", f32), ("momentum", f32), ("pad1", f32),
+    ]
+
+
+class HeadDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", vp), ("gx", vp), ("gout", vp), ("out", vp), ("pooled", vp),
+        ("x_ld", i64), ("gx_ld", i64),
+        ("n", i32), ("h", i32), ("w", i32), ("c", i32),
+        ("pool", i32), ("dtype", i32), ("beta", i32), ("pad0", i32),
+    ]
+
+
+class SoftmaxDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", vp), ("y", vp), ("gy", vp), ("gx", vp),
+        ("sn", i64), ("sc", i64), ("sh", i64), ("sw", i64),
+        ("n", i32), ("c", i32), ("h", i32), ("w", i32),
+        ("beta", i32), ("pad0", i32),
+    ]
+
+
 class PackList(ctypes.Structure):
     _fields_ = [("descs_dev", vp), ("n", i32), ("max_elems", i32)]
 
@@ -120,7 +150,7 @@ class PackList(ctypes.Structure):
 class _OpUnion(ctypes.Union):
     _fields_ = [
         ("conv", ConvDesc), ("wgrad", WgradDesc), ("wreduce", WreduceDesc), ("colsum", ColsumDesc),
-        ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList),
+        ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList), ("bn", BnDesc), ("head", HeadDesc),
     ]
 
 
@@ -129,13 +159,15 @@ class Op(ctypes.Structure):
 
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
-        OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, 100: WarpDesc}
+        OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
+        100: WarpDesc, 101: SoftmaxDesc}
 
 EXPORTS = [
     "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
     "dvie_ew", "dvie_loss", "dvie_loss_partial_count", "dvie_loss_ws_floats", "dvie_warp_fwd",
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
-    "dvie_last_error",
+    "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
+    "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam",
 ]
 
 _lib = None
@@ -168,11 +200,12 @@ def load():
         lib.dvie_version.restype = ctypes.c_char_p
         lib.dvie_last_error.restype = ctypes.c_char_p
         for name in ("dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_ew",
-                     "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd"):
+                     "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_head_fwd",
+                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd"):
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]
-        for name in ("dvie_wgrad_splits_hint", "dvie_wgrad_slabs"):
+        for name in ("dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_bn_partial_splits"):
             getattr(lib, name).argtypes = [vp]
             getattr(lib, name).restype = i32
         lib.dvie_run_ops.argtypes = [vp, i32, vp]
@@ -182,6 +215,7 @@ def load():
         lib.dvie_loss_ws_floats.restype = ctypes.c_size_t
         lib.dvie_adamax.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
         lib.dvie_scale.argtypes = [vp, i64, f32, vp]
+        lib.dvie_adam.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
         _lib = lib
         return lib
 

@@ -182,6 +182,10 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
       case DVIE_OP_EW: rc = dvie_ew(&o.u.ew, stream); break;
       case DVIE_OP_LOSS: rc = dvie_loss(&o.u.loss, stream); break;
       case DVIE_OP_PACK: rc = dvie_pack_weights(o.u.pack.descs_dev, o.u.pack.n, o.u.pack.max_elems, stream); break;
+      case DVIE_OP_BN_FWD: rc = dvie_bn_fwd(&o.u.bn, stream); break;
+      case DVIE_OP_BN_BWD: rc = dvie_bn_bwd(&o.u.bn, stream); break;
+      case DVIE_OP_HEAD_FWD: rc = dvie_head_fwd(&o.u.head, stream); break;
+      case DVIE_OP_HEAD_BWD: rc = dvie_head_bwd(&o.u.head, stream); break;
       default: set_error("run_ops: unknown op kind %d at %d", o.kind, i); return DVIE_EINVAL;
     }
     if (rc != DVIE_OK) {
@@ -207,7 +211,10 @@ size_t dvie_abi_sizeof(int which) {
     case DVIE_OP_EW: return sizeof(dvie_ew_desc);
     case DVIE_OP_LOSS: return sizeof(dvie_loss_desc);
     case DVIE_OP_PACK: return sizeof(dvie_pack_desc);
+    case DVIE_OP_BN_FWD: return sizeof(dvie_bn_desc);
+    case DVIE_OP_HEAD_FWD: return sizeof(dvie_head_desc);
     case 100: return sizeof(dvie_warp_desc);
+    case 101: return sizeof(dvie_softmax_desc);
     default: return 0;
   }
 }

@@ -196,6 +196,27 @@ class L1FeatOp(_Op):
         return [self.a]
 
 
+class BNOp(_Op):
+    """BatchNorm2d (+ activation) of a conv output buffer (reference nn.BatchNorm2d in
+    nets/FrameDisc.py / nets/VidDisc.py / VAEHRNet).  x must be read by this op only."""
+
+    def __init__(self, x, module, out, act, trainable):
+        self.x, self.m, self.out, self.act, self.trainable = x, module, out, act, trainable
+
+    def inputs(self):
+        return [self.x]
+
+
+class HeadOp(_Op):
+    """AvgPool2d(pool) + view(-1, C).mean(1) -> external fp32 vector `key`."""
+
+    def __init__(self, x, pool, key):
+        self.x, self.pool, self.key, self.out, self.act = x, pool, key, None, L.ACT_NONE
+
+    def inputs(self):
+        return [self.x]
+
+
 _IMAGENET_MEAN = [0.485, 0.456, 0.406]
 _IMAGENET_STD = [0.229, 0.224, 0.225]
 
@@ -252,6 +273,18 @@ class Graph:
         assert (out.H * 2, out.W * 2, out.c) == (x.H, x.W, x.c)
         self._add(PoolOp(x, out))
         return out
+
+    def bn(self, x, module, out, act=L.ACT_NONE, trainable=True):
+        assert (x.H, x.W, x.c) == (out.H, out.W, out.c) and x.c == rup(module.num_features, PADC)
+        self._add(BNOp(x, module, out, act, trainable))
+        return out
+
+    def head(self, x, pool, key):
+        assert x.H >= pool and x.W >= pool
+        self._add(HeadOp(x, pool, key))
+        self.heads = getattr(self, "heads", {})
+        self.heads[key] = x
+        return key
 
     def l1feat(self, a, weight=1.0):
         op = L1FeatOp(a, self.n_l1, weight)
@@ -322,6 +355,8 @@ class Plan:
                     need = op.requires_grad
                 elif isinstance(op, ConvOp):
                     need = op.layer.trainable or any(r.buf.needs_grad for r in op.inputs())
+                elif isinstance(op, BNOp):
+                    need = op.trainable or op.x.buf.needs_grad
                 else:
                     need = any(r.buf.needs_grad for r in op.inputs())
                 op.out.buf.needs_grad = op.out.buf.needs_grad or need
@@ -342,6 +377,19 @@ class Plan:
                         assert r.buf.read_region == r.key(), f"{r.buf}: consumers read different regions"
         self.l1_out = torch.zeros(max(1, g.n_l1), dtype=torch.float32, device=self.device)
         self.keep.append(self.l1_out)
+        self.bn_splits = 1
+        for op in g.ops:
+            if isinstance(op, BNOp):
+                d = L.BnDesc()
+                d.rows = self.nf * op.x.H * op.x.W
+                self.bn_splits = max(self.bn_splits, L.load().dvie_bn_partial_splits(ctypes.byref(d)))
+                d.rows = self.nb * op.x.H * op.x.W
+                self.bn_splits = max(self.bn_splits, L.load().dvie_bn_partial_splits(ctypes.byref(d)))
+                op.stats = torch.zeros((8, op.x.c), dtype=torch.float32, device=self.device)
+                self.keep.append(op.stats)
+        maxc = max([op.x.c for op in g.ops if isinstance(op, BNOp)] + [4])
+        self.bn_partial = torch.zeros(self.bn_splits * 2 * maxc, dtype=torch.float64, device=self.device)
+        self.keep.append(self.bn_partial)
 
     def ptr(self, region, n0=0, grad=False):
         b = region.buf
@@ -487,6 +535,26 @@ class Plan:
                 x, out = op.x, op.out
                 self.fwd.append(self.ew_desc(L.EW_POOL, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C,
                                              [(self.ptr(x), x.buf.C, x.H, x.W)]))
+            elif isinstance(op, BNOp):
+                o = self._op(L.OP_BN_FWD)
+                self._bn_common(o.u.bn, op, nf)
+                o.u.bn.y, o.u.bn.y_ld = self.ptr(op.out), op.out.buf.C
+                op.fwd_index = len(self.fwd)
+                self.bn_ops = getattr(self, "bn_ops", []) + [op]
+                self.fwd.append(o)
+            elif isinstance(op, HeadOp):
+                x = op.x
+                o = self._op(L.OP_HEAD_FWD)
+                d = o.u.head
+                d.x, d.x_ld = self.ptr(x), x.buf.C
+                d.n, d.h, d.w, d.c, d.pool, d.dtype = nf, x.H, x.W, x.c, op.pool, self.dt
+                rows = nf * (x.H // op.pool) * (x.W // op.pool)
+                op.pooled = torch.zeros(rows * x.c, dtype=torch.float32, device=self.device)
+                self.keep.append(op.pooled)
+                d.pooled = op.pooled.data_ptr()
+                self.ext_head = getattr(self, "ext_head", {})
+                self.ext_head[op.key] = (len(self.fwd), rows)
+                self.fwd.append(o)
             elif isinstance(op, L1FeatOp):
                 a = op.a
                 half = nf // 2
@@ -506,6 +574,23 @@ class Plan:
                 self.fwd.append(o)
             else:
                 raise TypeError(op)
+
+    def _bn_common(self, d, op, n):
+        x, m = op.x, op.m
+        d.x, d.x_ld = self.ptr(x), x.buf.C
+        d.rows, d.c = n * x.H * x.W, x.c
+        d.splits = L.load().dvie_bn_partial_splits(ctypes.byref(d))
+        d.partial, d.stats = self.bn_partial.data_ptr(), op.stats.data_ptr()
+        d.gamma = m.weight.data_ptr() if m.weight is not None else None
+        d.beta = m.bias.data_ptr() if m.bias is not None else None
+        d.running_mean = m.running_mean.data_ptr() if m.running_mean is not None else None
+        d.running_var = m.running_var.data_ptr() if m.running_var is not None else None
+        assert m.num_features == x.c or rup(m.num_features, PADC) == x.c
+        assert m.num_features == x.c, "BatchNorm channel count must be a multiple of 8"
+        d.training = int(getattr(self.g, "bn_training", True))
+        d.act, d.alpha, d.eps = op.act, 0.2, m.eps
+        d.momentum = m.momentum if m.momentum is not None else 0.0
+        d.dtype = self.dt
 
     # ---------------- backward ----------------
     def _contrib(self, region, emitter, ident=None):
@@ -584,6 +669,24 @@ class Plan:
             b.done = True
             b.dact_done = True
         for op in reversed(g.ops):
+            if isinstance(op, HeadOp):
+                x = op.x
+                if not x.buf.needs_grad:
+                    continue
+                xg = self.ptr(x, grad=True)
+
+                def em(beta, res, res_ld, dact, z, z_ld, op=op, x=x, xg=xg):
+                    assert res is None and dact == 0, "head backward has no fused epilogue"
+                    o = self._op(L.OP_HEAD_BWD)
+                    d = o.u.head
+                    d.gx, d.gx_ld = xg, x.buf.C
+                    d.n, d.h, d.w, d.c, d.pool, d.dtype, d.beta = nb, x.H, x.W, x.c, op.pool, self.dt, beta
+                    self.ext_head_grad = getattr(self, "ext_head_grad", {})
+                    self.ext_head_grad[op.key] = len(self.bwd)
+                    return [o]
+
+                self._contrib(x, em)
+                continue
             if isinstance(op, L1FeatOp):
                 a = op.a
                 if not a.buf.needs_grad:
@@ -616,6 +719,24 @@ class Plan:
                 continue
             if isinstance(op, ConvOp):
                 self._conv_backward(op, gout, gld)
+            elif isinstance(op, BNOp):
+                x = op.x
+                assert len(x.buf.consumers) == 1, "BatchNorm input must have no other reader"
+                xg = self.ptr(x, grad=True) if x.buf.needs_grad else None
+                if x.buf.needs_grad:
+                    def em(beta, res, res_ld, dact, z, z_ld, op=op, x=x, xg=xg, gout=gout, gld=gld):
+                        assert res is None and dact == 0, "BatchNorm backward has no fused epilogue"
+                        o = self._op(L.OP_BN_BWD)
+                        d = o.u.bn
+                        self._bn_common(d, op, nb)
+                        d.g, d.g_ld = gout, gld
+                        d.dx, d.dx_ld, d.beta_dx = xg, x.buf.C, beta
+                        if op.trainable:
+                            self._grad_slots.append((len(self.bwd), op.m, "bn", op.m not in self.wg_first))
+                            self.wg_first[op.m] = True
+                        return [o]
+
+                    self._contrib(x, em)
             elif isinstance(op, FuseOp):
                 for s in op.srcs:
                     if not s.buf.needs_grad:
@@ -772,6 +893,18 @@ class Plan:
             d.y = t.data_ptr() + region.c0 * t.element_size()
             d.y_ld = t.shape[-1]
 
+    def set_head_output(self, key, t):
+        """Point head `key` at an fp32 vector of length n*(h/pool)*(w/pool)."""
+        idx, rows = self.ext_head[key]
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == rows
+        self.fwd_arr[idx + self.fwd_off].u.head.out = t.data_ptr()
+
+    def set_head_grad(self, key, t):
+        t = t.contiguous()
+        assert t.dtype == torch.float32
+        self.bwd_arr[self.ext_head_grad[key]].u.head.gout = t.data_ptr()
+        self.keep_grad = t
+
     def set_output_grad(self, key, t):
         """Patch the incoming gradient (fp32, any strides, logical NCHW) of output `key`."""
         assert t.dtype == torch.float32
@@ -791,6 +924,17 @@ class Plan:
     def set_param_grads(self, accumulate=False):
         """Point weight reductions at the parameters' .grad tensors (fp32, OIHW)."""
         for idx, lay, which, first in self._grad_slots:
+            if which == "bn":  # lay is the BatchNorm module: gamma and beta gradients
+                d = self.bwd_arr[idx].u.bn
+                for pname, field in (("weight", "dgamma"), ("bias", "dbeta")):
+                    p = getattr(lay, pname)
+                    if p is None:
+                        continue
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+                    setattr(d, field, p.grad.data_ptr())
+                d.accumulate = int(accumulate) if first else 1
+                continue
             p = getattr(lay.m, which)
             if p.grad is None:
                 p.grad = torch.zeros_like(p)

@@ -4,3 +4,5 @@ from .ExtraNet import ExtraNet
 from .HRNet import HRNet
 from .InterNet import InterNet
 from .vgg import VGG19, my_vgg, vgg19_features
+from .disc import FrameDiscriminator, ResnetBlock, VideoDiscriminator
+from .InterGANNet import InterGANNet, channel_softmax

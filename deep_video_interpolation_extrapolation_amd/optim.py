@@ -1,27 +1,38 @@
-"""Adamax on libdvie (reference optimizer: torch.optim.Adamax, runners/InterTrainer.py:79).
+"""Fused optimizers on libdvie.
 
-Same constructor, param_groups and state_dict layout as torch.optim.Adamax (per-parameter
-state {'step', 'exp_avg', 'exp_inf'}), so checkpoints interchange.  When a group's
-parameters are exactly the views of one FlatParams buffer (the HRNet case) and their
-.grad tensors are views of its flat gradient, the whole group updates in ONE fused HIP
-kernel over the flat buffers (state tensors are views of two flat state buffers);
-otherwise one fused-kernel launch per parameter.
+* `Adamax`: the generator optimizer (torch.optim.Adamax, runners/InterTrainer.py:79).
+* `Adam`: the discriminator optimizers (torch.optim.Adam, runners/InterGANTrainer.py:110-112),
+  torch 1.0.1 update form (eps added to sqrt(v) before the bias-correction scaling).
+
+Same constructors, param_groups and state_dict layouts as torch.optim (per-parameter state
+{'step', 'exp_avg', 'exp_inf'} / {'step', 'exp_avg', 'exp_avg_sq'}), so checkpoints
+interchange.  When a group's parameters are exactly the views of one FlatParams buffer
+(HRNet, the discriminators) and their .grad tensors are views of its flat gradient, the
+whole group updates in ONE fused HIP kernel over the flat buffers (state tensors are views
+of two flat state buffers); otherwise one fused-kernel launch per parameter.
 """
+import math
+
 import torch
 
 from . import _lib as L
 
 
-class Adamax(torch.optim.Optimizer):
-    def __init__(self, params, lr=2e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0):
+class _FusedOptimizer(torch.optim.Optimizer):
+    STATE = ("exp_avg", "exp_inf")
+
+    def __init__(self, params, lr, betas, eps, weight_decay):
         if not 0.0 <= lr:
             raise ValueError(f"Invalid learning rate: {lr}")
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self._flat = {}
 
+    def _launch(self, p, g, s0, s1, n, group, step, device):
+        raise NotImplementedError
+
     def _flat_group(self, gi, group):
-        """(owner, flat state m, flat state u) if the group maps onto one flat buffer."""
+        """(owner, flat state 0, flat state 1) if the group maps onto one flat buffer."""
         ps = group["params"]
         owner = getattr(ps[0], "_dvie_owner", None) if ps else None
         if owner is None or any(getattr(p, "_dvie_owner", None) is not owner for p in ps):
@@ -36,6 +47,7 @@ class Adamax(torch.optim.Optimizer):
             g = p.grad
             if g is None or g.data_ptr() != fg.data_ptr() + (p.data_ptr() - flat.data_ptr()):
                 return None
+        k0, k1 = self.STATE
         ent = self._flat.get(gi)
         if ent is None or ent[1].device != flat.device or ent[1].numel() != flat.numel():
             m = torch.zeros_like(flat)
@@ -43,11 +55,11 @@ class Adamax(torch.optim.Optimizer):
             for p in ps:
                 off = (p.data_ptr() - flat.data_ptr()) // 4
                 st = self.state[p]
-                if "exp_avg" in st:  # e.g. after load_state_dict
-                    m[off:off + p.numel()].copy_(st["exp_avg"].reshape(-1))
-                    u[off:off + p.numel()].copy_(st["exp_inf"].reshape(-1))
-                st["exp_avg"] = m[off:off + p.numel()].view_as(p)
-                st["exp_inf"] = u[off:off + p.numel()].view_as(p)
+                if k0 in st:  # e.g. after load_state_dict
+                    m[off:off + p.numel()].copy_(st[k0].reshape(-1))
+                    u[off:off + p.numel()].copy_(st[k1].reshape(-1))
+                st[k0] = m[off:off + p.numel()].view_as(p)
+                st[k1] = u[off:off + p.numel()].view_as(p)
                 st.setdefault("step", torch.tensor(0.0))
             ent = (owner, m, u)
             self._flat[gi] = ent
@@ -59,41 +71,61 @@ class Adamax(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        lib = L.load()
+        k0, k1 = self.STATE
         for gi, group in enumerate(self.param_groups):
-            b1, b2 = group["betas"]
-            eps, wd, lr = group["eps"], group["weight_decay"], group["lr"]
             flat = self._flat_group(gi, group)
             if flat is not None:
                 owner, m, u = flat
                 ps = group["params"]
-                st0 = self.state[ps[0]]
-                step = float(st0["step"]) + 1
+                step = float(self.state[ps[0]]["step"]) + 1
                 for p in ps:
                     self.state[p]["step"] = torch.tensor(step)
-                clr = lr / (1 - b1 ** step)
-                L.check(lib.dvie_adamax(owner._flat.data_ptr(), owner._flat_grad.data_ptr(), m.data_ptr(),
-                                        u.data_ptr(), owner._flat.numel(), clr, b1, b2, eps, wd,
-                                        L.stream_ptr(owner._flat.device)), "adamax")
+                self._launch(owner._flat, owner._flat_grad, m, u, owner._flat.numel(), group, step,
+                             owner._flat.device)
                 continue
             for p in group["params"]:
                 if p.grad is None:
                     continue
                 L.require_gpu(p)
                 st = self.state[p]
-                if len(st) == 0 or "exp_avg" not in st:
+                if len(st) == 0 or k0 not in st:
                     st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_inf"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st[k0] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st[k1] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
-                clr = lr / (1 - b1 ** float(st["step"]))
                 g = p.grad.contiguous()
-                assert p.is_contiguous() and st["exp_avg"].is_contiguous()
-                L.check(lib.dvie_adamax(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
-                                        st["exp_inf"].data_ptr(), p.numel(), clr, b1, b2, eps, wd,
-                                        L.stream_ptr(p.device)), "adamax")
+                assert p.is_contiguous() and st[k0].is_contiguous()
+                self._launch(p, g, st[k0], st[k1], p.numel(), group, float(st["step"]), p.device)
         return loss
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._flat = {}  # re-bind flat state views (copies loaded values in _flat_group)
+
+
+class Adamax(_FusedOptimizer):
+    STATE = ("exp_avg", "exp_inf")
+
+    def __init__(self, params, lr=2e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0):
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+    def _launch(self, p, g, s0, s1, n, group, step, device):
+        b1, b2 = group["betas"]
+        clr = group["lr"] / (1 - b1 ** step)
+        L.check(L.load().dvie_adamax(p.data_ptr(), g.data_ptr(), s0.data_ptr(), s1.data_ptr(), n, clr, b1, b2,
+                                     group["eps"], group["weight_decay"], L.stream_ptr(device)), "adamax")
+
+
+class Adam(_FusedOptimizer):
+    STATE = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("amsgrad (unused by the reference)")
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+    def _launch(self, p, g, s0, s1, n, group, step, device):
+        b1, b2 = group["betas"]
+        step_size = group["lr"] * math.sqrt(1 - b2 ** step) / (1 - b1 ** step)
+        L.check(L.load().dvie_adam(p.data_ptr(), g.data_ptr(), s0.data_ptr(), s1.data_ptr(), n, step_size, b1, b2,
+                                   group["eps"], group["weight_decay"], L.stream_ptr(device)), "adam")

@@ -151,6 +151,10 @@ class InterTrainer:
     def normalize(self, img):
         return (img + 1) / 2
 
+    def _predict(self, x, seg, gt_x, gt_seg):
+        out = self.model(x, seg=seg)
+        return out[0], out[1]
+
     def validate(self):
         self.log.info("Validation epoch {} started".format(self.epoch))
         self.model.eval()
@@ -160,7 +164,7 @@ class InterTrainer:
             for i, data in enumerate(self.val_loader):
                 data = batch_to(data, self.device)
                 x, seg, gt_x, gt_seg = self.get_input(data)
-                coarse_img, coarse_seg = self.model(x, seg=seg)
+                coarse_img, coarse_seg = self._predict(x, seg, gt_x, gt_seg)
                 coarse_img = coarse_img.clamp(-1, 1)
                 a, b = self.normalize(coarse_img), self.normalize(gt_x)
                 d = OrderedDict()

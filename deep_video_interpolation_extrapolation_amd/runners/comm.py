@@ -35,10 +35,16 @@ class GradSync:
         self.W = world()
         self.bucket_bytes = int(float(bucket_mb or os.environ.get("DVIE_BUCKET_MB", 16)) * 2 ** 20)
         self.flat_owners = [m for m in module.modules() if hasattr(m, "_flat")]
+        # owners that launch their buckets from inside their backward (HRNet); the others
+        # (discriminators, a few MB, gradients accumulated over two plan backwards) get one
+        # all-reduce of their flat gradient after the backward
+        self.hooked = [m for m in self.flat_owners if hasattr(m, "_buckets")]
+        self.post = [m for m in self.flat_owners if not hasattr(m, "_buckets")]
         self.works = []
         if self.W > 1:
             for m in self.flat_owners:  # DDP's initial parameter broadcast
                 dist.broadcast(m._flat, 0)
+            for m in self.hooked:
                 m.grad_hook = (self.bucket_bytes, self._make_hook(m))
 
     def _make_hook(self, owner):
@@ -63,6 +69,9 @@ class GradSync:
         """Wait for the bucket all-reduces and apply the 1/W factor (HIP kernel)."""
         if self.W == 1:
             return
+        for m in self.post:
+            if m._flat_grad is not None and any(p.grad is not None for p in m.parameters()):
+                self.works.append(dist.all_reduce(m._flat_grad, op=dist.ReduceOp.SUM, async_op=True))
         self.wait()
         lib = L.load()
         for m in self.flat_owners:

@@ -288,6 +288,92 @@ int dvie_adamax(float* p, const float* g, float* m, float* u, long long n, float
 int dvie_scale(float* p, long long n, float s, void* stream);
 
 /*
+ * BatchNorm2d over NHWC rows (rows = N*H*W pixels, c channels), fused with the following
+ * activation (nets/FrameDisc.py:45-46, nets/VidDisc.py:45-50, nets/HRNet.py:726-789).
+ * training = 1: batch statistics (biased variance for the normalisation; running_mean /
+ * running_var, if non-NULL, updated with `momentum` and the unbiased variance, as
+ * nn.BatchNorm2d.train()); training = 0: running statistics.
+ *   forward : y = act(gamma * (x - mean) * invstd + beta)
+ *   backward: g = dL/d(pre-activation output) (the engine applies act' upstream);
+ *             dgamma (+)= sum g*xhat, dbeta (+)= sum g (accumulate selects +=);
+ *             dx (+)= gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)) (beta_dx selects +=).
+ * partial: double [splits][2][c] workspace (splits = dvie_bn_partial_splits); stats: fp32
+ * [8][c] per-call state written by the forward and read by the backward.
+ * Constraints: c % 4 == 0, c <= 1024, lds % 4 == 0.
+ */
+typedef struct dvie_bn_desc {
+  const void* x;
+  void* y;
+  const void* g;
+  void* dx;
+  const float* gamma;
+  const float* beta;
+  float* dgamma;
+  float* dbeta;
+  float* running_mean;
+  float* running_var;
+  double* partial;
+  float* stats;
+  long long x_ld, y_ld, g_ld, dx_ld;
+  long long rows;
+  int c, splits, act, training;
+  int dtype, accumulate, beta_dx, pad0;
+  float alpha, eps, momentum, pad1;
+} dvie_bn_desc;
+
+int dvie_bn_fwd(const dvie_bn_desc* d, void* stream);
+int dvie_bn_bwd(const dvie_bn_desc* d, void* stream);
+int dvie_bn_partial_splits(const dvie_bn_desc* d);
+
+/*
+ * Discriminator head: AvgPool2d(pool) of an NHWC (n, h, w, c) map, then
+ * view(-1, c).mean(1) over the NCHW-flat pooled tensor (nets/FrameDisc.py:66,74;
+ * nets/VidDisc.py:77,83): out[r] = mean(pooled_nchw[r*c : (r+1)*c]), r < n*(h/pool)*(w/pool).
+ * pooled: fp32 workspace of n*c*(h/pool)*(w/pool).  Backward: gx (+)= the adjoint applied
+ * to gout (pixels past the floor(h/pool)*pool crop get 0).
+ */
+typedef struct dvie_head_desc {
+  const void* x;
+  void* gx;
+  const float* gout;
+  float* out;
+  float* pooled;
+  long long x_ld, gx_ld;
+  int n, h, w, c;
+  int pool, dtype, beta, pad0;
+} dvie_head_desc;
+
+int dvie_head_fwd(const dvie_head_desc* d, void* stream);
+int dvie_head_bwd(const dvie_head_desc* d, void* stream);
+
+/*
+ * Channel softmax (F.softmax(seg, dim=1), nets/InterGANNet.py:40), fp32: x with NCHW
+ * strides (sn, sc, sh, sw) in elements, y contiguous NCHW.  Backward (gy, y contiguous):
+ * gx (+)= y * (gy - sum_c gy*y).
+ */
+typedef struct dvie_softmax_desc {
+  const float* x;
+  float* y;
+  const float* gy;
+  float* gx;
+  long long sn, sc, sh, sw;
+  int n, c, h, w;
+  int beta, pad0;
+} dvie_softmax_desc;
+
+int dvie_softmax_fwd(const dvie_softmax_desc* d, void* stream);
+int dvie_softmax_bwd(const dvie_softmax_desc* d, void* stream);
+
+/*
+ * Fused Adam over a flat fp32 buffer, torch 1.0.1 update form (the discriminator
+ * optimizers, runners/InterGANTrainer.py:110-112): m = b1*m + (1-b1)*g;
+ * v = b2*v + (1-b2)*g^2; p -= step_size * m / (sqrt(v) + eps) with
+ * step_size = lr*sqrt(1-b2^t)/(1-b1^t) computed by the caller; weight decay g += wd*p first.
+ */
+int dvie_adam(float* p, const float* g, float* m, float* v, long long n, float step_size, float b1, float b2,
+              float eps, float wd, void* stream);
+
+/*
  * Op-list executor: runs n descriptors in order on one stream with a single host call
  * (the per-step forward and backward plans of the HRNet / VGG executors).
  */
@@ -298,6 +384,10 @@ int dvie_scale(float* p, long long n, float s, void* stream);
 #define DVIE_OP_EW 5
 #define DVIE_OP_LOSS 6
 #define DVIE_OP_PACK 7
+#define DVIE_OP_BN_FWD 8
+#define DVIE_OP_BN_BWD 9
+#define DVIE_OP_HEAD_FWD 10
+#define DVIE_OP_HEAD_BWD 11
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
@@ -315,6 +405,8 @@ typedef struct dvie_op {
     dvie_ew_desc ew;
     dvie_loss_desc loss;
     dvie_pack_list pack;
+    dvie_bn_desc bn;
+    dvie_head_desc head;
   } u;
 } dvie_op;
 

@@ -75,3 +75,75 @@ def extra_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(8
     for k, v in ld.items():
         ren["step_1_frame_1_" + k if k.startswith("coarse") else k] = v
     return ren, grads, new, state, outs
+
+
+def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats, lr=1e-3, disc_lr=1e-3,
+             w_rgb=(80.0, 80.0, 20.0, 20.0), w_ce=30.0, w_d=1.0, w_g=1.0, state=None):
+    """One InterGANTrainer step (reference runners/InterGANTrainer.py:359-456 with
+    nets/InterGANNet.py:28-117), HRNet coarse model (mu = logvar = None, no KLD), frame and
+    video discriminators with seg_disc.  Returns (loss dict, new generator params, new frame
+    disc params, new video disc params, states)."""
+    from . import disc as D
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+    Pf = {k: v.detach().clone().requires_grad_(True) for k, v in frame_p.items()}
+    Pv = {k: v.detach().clone().requires_grad_(True) for k, v in video_p.items()}
+    gt_x, gt_seg = data["frame2"], data["seg2"]
+    x = torch.cat([data["frame1"], data["frame3"]], 1)
+    seg = torch.cat([data["seg1"], data["seg3"]], 1)
+    rgb, seg_out = hrnet.forward(P, torch.cat([x, seg], 1))
+    soft = torch.softmax(seg_out, dim=1)
+    FS, VS = D.FRAME(23), D.VIDEO(23)
+    df_fake = D.forward(Pf, FS, torch.cat([rgb.detach(), soft.detach()], 1), stats=frame_stats)
+    df_real = D.forward(Pf, FS, torch.cat([gt_x, gt_seg], 1), stats=frame_stats)
+    dv_fake = D.forward(Pv, VS, torch.cat([rgb.detach(), soft.detach(), x, seg], 1), stats=video_stats)
+    dv_real = D.forward(Pv, VS, torch.cat([gt_x, gt_seg, x, seg], 1), stats=video_stats)
+    gf = D.forward({k: v.detach() for k, v in Pf.items()}, FS, torch.cat([rgb, soft], 1), stats=frame_stats)
+    gv = D.forward({k: v.detach() for k, v in Pv.items()}, VS, torch.cat([rgb, soft, x, seg], 1), stats=video_stats)
+    ld = losses.rgb_loss(vgg_state, (rgb + 1) / 2, (gt_x + 1) / 2, normed=False, w=w_rgb)
+    ld["coarse_ce_loss"] = w_ce * losses.seg_ce(seg_out, gt_seg)
+    ld["coarse_frame_loss"] = D.gan_scalar_loss(gf, w_g, True)
+    ld["disc_frame_real_loss"] = D.gan_scalar_loss(df_real, w_d, True)
+    ld["disc_frame_fake_loss"] = D.gan_scalar_loss(df_fake, w_d, False)
+    ld["coarse_video_loss"] = D.gan_scalar_loss(gv, w_g, True)
+    ld["disc_video_real_loss"] = D.gan_scalar_loss(dv_real, w_d, True)
+    ld["disc_video_fake_loss"] = D.gan_scalar_loss(dv_fake, w_d, False)
+    loss = 0
+    for v in ld.values():
+        loss = loss + torch.mean(v)
+    ld["loss_all"] = loss
+    loss.backward()
+    st = state or {}
+    new, st["g"] = adamax(params, {k: v.grad for k, v in P.items()}, lr, st.get("g"))
+    newf, st["f"] = D.adam_101(frame_p, {k: v.grad for k, v in Pf.items()}, disc_lr, st.get("f"))
+    newv, st["v"] = D.adam_101(video_p, {k: v.grad for k, v in Pv.items()}, disc_lr, st.get("v"))
+    grads = {"g": {k: v.grad for k, v in P.items()}, "f": {k: v.grad for k, v in Pf.items()},
+             "v": {k: v.grad for k, v in Pv.items()}}
+    return OrderedDict((k, float(v)) for k, v in ld.items()), new, newf, newv, st, grads
+
+
+def extra_rollout_step(params, vgg_state, data, nps=2, lr=1e-3, weights=(80.0, 80.0, 20.0, 20.0, 30.0)):
+    """ExtraTrainer step with num_pred_step = nps > 1, num_pred_once = 1: the rollout the
+    reference intends at runners/ExtraTrainer.py:304-310 (whose `out_img` / `out_seg` are
+    undefined names): next input = [x[:, -3:], prediction] / [seg[:, -20:],
+    onehot(argmax(seg prediction))], gradients flowing back through the prediction."""
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+    last_rgb = torch.cat([data["frame1"], data["frame2"]], 1)
+    last_seg = torch.cat([data["seg1"], data["seg2"]], 1)
+    ld = OrderedDict()
+    for ii in range(nps):
+        gt, gseg = data[f"frame{3 + ii}"], data[f"seg{3 + ii}"]
+        rgb, seg_out = hrnet.forward(P, torch.cat([last_rgb, last_seg], 1))
+        prefix = f"step_{ii + 1}_frame_1_coarse"
+        ld.update(losses.rgb_loss(vgg_state, rgb, gt, normed=False, w=weights[:4], prefix=prefix))
+        ld[prefix + "_ce_loss"] = weights[4] * losses.seg_ce(seg_out, gseg)
+        last_rgb = torch.cat([last_rgb[:, -3:], rgb], 1)
+        oh = torch.nn.functional.one_hot(seg_out.argmax(1), 20).permute(0, 3, 1, 2).float()
+        last_seg = torch.cat([last_seg[:, -20:], oh], 1)
+    loss = 0
+    for v in ld.values():
+        loss = loss + torch.mean(v)
+    ld["loss_all"] = loss
+    loss.backward()
+    grads = {k: v.grad.detach().clone() for k, v in P.items()}
+    new, state = adamax(params, grads, lr)
+    return OrderedDict((k, float(v)) for k, v in ld.items()), grads, new

@@ -67,3 +67,20 @@ def step_batch(n, H, W):
             lab = torch.randint(0, 20, (H, W), generator=g)
             out[f"seg{k}"].append(torch.nn.functional.one_hot(lab, 20).permute(2, 0, 1).float())
     return {k: torch.stack(v) for k, v in out.items()}
+
+
+def disc_inputs(n=2, H=128, W=256, seed=21):
+    """frame disc (x, seg) and video disc extra (input_x, input_seg); upstream score grads."""
+    g = _gen(seed)
+    x = torch.rand((n, 3, H, W), generator=g) * 2 - 1
+    seg = torch.softmax(torch.randn((n, 20, H, W), generator=g) * 2, dim=1)
+    ix = torch.rand((n, 6, H, W), generator=g) * 2 - 1
+    iseg = torch.cat([onehot(torch.randint(0, 20, (n, H, W), generator=g)) for _ in range(2)], 1)
+    k = (H // 128) * (W // 128)
+    gout = torch.randn((n * k,), generator=g)
+    return x, seg, ix, iseg, gout
+
+
+def sample_idx(numel, k=256, seed=99):
+    """fixed sample positions for large-tensor fixtures"""
+    return torch.randint(0, numel, (k,), generator=_gen(seed))

@@ -12,6 +12,10 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
                      as InterTrainer calls it) and [0,1] inputs; CE
   warp.npz       G3: reference FlowWrapper forward/backward (align_corners=True)
   metrics.npz    G5: reference PSNR / SSIM / IoU / VGGCosineLoss
+  disc.npz       G6: reference FrameDiscriminator / VideoDiscriminator (seg_disc, BatchNorm
+                     in train mode) at 128x128 and 128x256 (NCHW-flat head grouping): scores,
+                     input gradients, parameter-gradient stats, running statistics, hinge
+                     losses, eval-mode scores
   step.npz       G4: one training step of the reference modules (InterTrainer.py:380-441
                      body): loss dict, per-parameter gradient stats, post-Adamax checksums
 """
@@ -140,7 +144,44 @@ def g4():
                         seg=coarse_seg.detach().numpy()[:, :, ::4, ::4])
 
 
+def g6():
+    out = {}
+    for tag, cls, seed in (("frame", "FrameDiscriminator", 31), ("video", "VideoDiscriminator", 32)):
+        for H, W in ((128, 128), (128, 256)):
+            t = f"{tag}_{H}x{W}"
+            torch.manual_seed(seed)
+            d = ref_nets.__dict__[cls](args_ns(seg_disc=True))
+            d.train()
+            x, seg, ix, iseg, gout = inputs.disc_inputs(2, H, W)
+            ins = [x, seg] + ([ix, iseg] if tag == "video" else [])
+            ins = [v.clone().requires_grad_(True) for v in ins]
+            score = d(*ins)
+            score.backward(gout)
+            out[t + "_score"] = score.detach().numpy()
+            for k, v in enumerate(ins):  # large: stats + seeded sample points (inputs.sample_idx)
+                gv = v.grad.double().reshape(-1)
+                out[t + f"_gin{k}"] = np.concatenate([[float(gv.sum()), float(gv.abs().sum()), float(gv.norm())],
+                                                      gv[inputs.sample_idx(gv.numel())].numpy()])
+            named = dict(d.named_parameters())
+            names = sorted(named)
+            out[t + "_param_names"] = np.array(names)
+            out[t + "_grad_stats"] = np.array([[float(named[n].grad.double().sum()),
+                                                float((named[n].grad.double() ** 2).sum())] for n in names])
+            bufs = {k: v for k, v in d.state_dict().items() if "running" in k}
+            out[t + "_buf_names"] = np.array(sorted(bufs))
+            out[t + "_bufs"] = np.concatenate([bufs[k].numpy() for k in sorted(bufs)])
+            gl = ref_losses.GANScalarLoss(weight=1.5)
+            out[t + "_hinge"] = np.array([gl(score, True).item(), gl(score, False).item()])
+            d.eval()
+            with torch.no_grad():
+                out[t + "_score_eval"] = d(*[v.detach() for v in ins]).numpy()
+    np.savez_compressed(os.path.join(HERE, "disc.npz"), **out)
+
+
 if __name__ == "__main__":
-    for f in (g1, g2, g3, g5, g4):
+    import sys as _sys
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6)}
+    for name in (_sys.argv[1:] or list(todo)):
+        f = todo[name]
         f()
         print("wrote", f.__name__)

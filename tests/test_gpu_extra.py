@@ -61,25 +61,57 @@ def test_hrnet_frames_input_gradient(dev, monkeypatch):
     rgb, s = m(xd, seg.to(dev))
     ((rgb * r1.to(dev)).sum() + (s * r2.to(dev)).sum()).backward()
     torch.cuda.synchronize()
-    P = O.init_params(1024)
-    xr = x.clone().requires_grad_(True)
-    rr, sr = O.forward(P, torch.cat([xr, seg], 1))
-    ((rr * r1).sum() + (sr * r2).sum()).backward()
-    err = float((xd.grad.cpu() - xr.grad).abs().max() / xr.grad.abs().max())
-    assert err < 1e-4, err
+    def oracle_grad(dt):
+        P = {k: v.to(dt) for k, v in O.init_params(1024).items()}
+        xr = x.to(dt).clone().requires_grad_(True)
+        rr, sr = O.forward(P, torch.cat([xr, seg.to(dt)], 1))
+        ((rr * r1.to(dt)).sum() + (sr * r2.to(dt)).sum()).backward()
+        return xr.grad.double()
+
+    g64, g32 = oracle_grad(torch.float64), oracle_grad(torch.float32)
+
+    def rel_l2(a):
+        return float((a - g64).norm() / g64.norm())
+
+    # The stem gradient is a long sum of cancelling terms through 77 layers: the fp32
+    # CPU oracle itself is only ~8e-4 (relative L2) from fp64 at this shape, and an
+    # activation within ~1e-8 of zero may take the other LeakyReLU branch (DESIGN.md
+    # "Numerics").  Gate: the HIP fp32 gradient is within 1e-2 relative L2 of fp64 and
+    # within 10x the oracle's own fp32 error (a wrong channel map or a missing term
+    # gives O(1) errors).
+    e_hip, e32 = rel_l2(xd.grad.cpu().double()), rel_l2(g32)
+    assert e_hip < 1e-2 and e_hip < 10 * max(e32, 1e-4), (e_hip, e32)
 
 
-@pytest.mark.parametrize("kw", [dict(num_pred_step=2), dict(num_pred_once=2, vid_length=2)])
-def test_extra_bf16_variants_train(dev, kw):
+def test_extra_rollout_step_matches_oracle(dev):
+    """num_pred_step = 2 (autoregressive rollout, gradients through the fed-back
+    prediction) fp32 step vs oracle.step.extra_rollout_step: loss dict 1e-4 relative;
+    post-Adamax sums of squares 1e-4 relative."""
     from deep_video_interpolation_extrapolation_amd.data import SyntheticClips
-    tr = extra_trainer("bf16", 64, 128, 2, **kw)
-    k = 2 + max(kw.get("vid_length", 1), kw.get("num_pred_step", 1))
-    ds = SyntheticClips(2, 64, 128, k)
+    tr = extra_trainer("fp32", 32, 64, 2, num_pred_step=2)
+    ds = SyntheticClips(2, 32, 64, 4)
+    items = [ds[i] for i in range(2)]
+    data = {key: torch.stack([it[key] for it in items]) for key in items[0]}
+    P = O.init_params(1024)
+    ld = tr.step(data)
+    ref, grads, new = OS.extra_rollout_step(P, OL.synthetic_vgg19_state(), data, nps=2)
+    assert list(ld.keys()) == list(ref.keys())
+    np.testing.assert_allclose([float(ld[k]) for k in ref], [ref[k] for k in ref], rtol=1e-4)
+    named = dict(tr.model.module.coarse_model.named_parameters())
+    post = np.array([float((named[n].detach().double() ** 2).sum()) for n in new])
+    want = np.array([float((new[n].double() ** 2).sum()) for n in new])
+    np.testing.assert_allclose(post, want, rtol=1e-4)
+
+
+def test_extra_multi_frame_bf16_trains(dev):
+    """num_pred_once = 2 (two frames per forward: 6 rgb + 40 seg output channels)."""
+    from deep_video_interpolation_extrapolation_amd.data import SyntheticClips
+    tr = extra_trainer("bf16", 64, 128, 2, num_pred_once=2, vid_length=2)
+    ds = SyntheticClips(2, 64, 128, 4)
     items = [ds[i] for i in range(2)]
     data = {key: torch.stack([it[key] for it in items]) for key in items[0]}
     losses = [float(tr.step(data)["loss_all"]) for _ in range(5)]
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses
     keys = list(tr.step(data).keys())
-    n = kw.get("num_pred_step", 1) * kw.get("num_pred_once", 1)
-    assert sum(k.endswith("_ce_loss") for k in keys) == n
+    assert sum(k.endswith("_ce_loss") for k in keys) == 2
