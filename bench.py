@@ -28,6 +28,11 @@ sys.path.insert(0, ROOT)
 PEAK_BF16_TFLOPS = 2500.0  # dense MFMA (MI355X_MICROARCH.md)
 PEAK_FP32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwise", 6: "loss", 7: "weight_pack",
+              8: "batchnorm_fwd", 9: "batchnorm_bwd", 10: "head_fwd", 11: "head_bwd"}
+# HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
+# this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01c_pmc", "traffic.json")
 
 
 def parse():
@@ -41,6 +46,7 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
+    ap.add_argument("--ops-out", default=None, help="write the per-op profile table (profiling steps) here")
     return ap.parse_args()
 
 
@@ -121,28 +127,55 @@ def main():
         torch.cuda.synchronize()
         engine.PROFILE = None
     agg = {}
+    per_op = {}
+    roof_t = {}  # per-op roofline time: max(F / P_mfma, B / BW_hbm)
+    peak = PEAK_BF16_TFLOPS if a.precision == "bf16" else PEAK_FP32_TFLOPS
     for meta, kind, e0, e1 in prof:
         ms = e0.elapsed_time(e1)
-        cls = meta["cls"] if meta else f"kind{kind}"
-        r = agg.setdefault(cls, dict(ms=0.0, n=0, flops=0.0, bytes=0.0))
+        cls = meta["cls"] if meta else KIND_NAMES.get(kind, f"kind{kind}")
+        r = agg.setdefault(cls, dict(ms=0.0, n=0, flops=0.0, bytes=0.0, roof_ms=0.0))
         r["ms"] += ms
         r["n"] += 1
         if meta:
-            r["flops"] += meta.get("flops", 0.0)
-            r["bytes"] += meta.get("bytes", 0.0)
+            f, b = meta.get("flops", 0.0), meta.get("bytes", 0.0)
+            r["flops"] += f
+            r["bytes"] += b
+            r["roof_ms"] += 1e3 * max(f / (peak * 1e12), b / (PEAK_HBM_GBS * 1e9))
+            o = per_op.setdefault((cls, meta.get("name", "?")), dict(ms=0.0, n=0, flops=0.0, bytes=0.0))
+            o["ms"] += ms
+            o["n"] += 1
+            o["flops"] += f
+            o["bytes"] += b
     conv = [agg[c] for c in ("conv_fwd", "conv_dgrad") if c in agg]
     roof = None
     if conv:
         ms = sum(r["ms"] for r in conv)
         n = sum(r["n"] for r in conv)
         fl = sum(r["flops"] for r in conv)
+        by = sum(r["bytes"] for r in conv)
         tf = fl / (ms * 1e-3) / 1e12
-        peak = PEAK_BF16_TFLOPS if a.precision == "bf16" else PEAK_FP32_TFLOPS
+        traffic = None
+        if os.path.exists(PMC_TRAFFIC):
+            t = json.load(open(PMC_TRAFFIC)).get("conv")
+            traffic = round(t["bytes_per_launch"]) if t else None
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
-                "traffic": None, "kernel": "conv_igemm_kernel (fwd + dgrad launches)",
+                "traffic": traffic, "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE, "
+                                                     "profiles/r01c_pmc)",
+                "algorithmic_bytes_per_launch": round(by / max(1, n)),
+                "kernel": "conv fwd+dgrad family (conv_halo / conv_ws / conv1x1 / conv_igemm kernels)",
                 "launches_per_step": n // max(1, a.profile_steps),
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
-                "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4)}
+                "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4),
+                # sum over launches of max(F/P_mfma, B/BW_hbm) over measured time
+                "per_op_roofline_time_frac": round(sum(r["roof_ms"] for r in conv) / ms, 4)}
+    if a.ops_out and rank == 0:
+        with open(a.ops_out, "w") as f:
+            f.write(f"{'class':12s} {'layer':42s} {'n':>3s} {'ms':>8s} {'TFLOP/s':>8s} {'GB/s':>8s} {'roof%':>6s}\n")
+            for (cls, name), o in sorted(per_op.items(), key=lambda kv: -kv[1]["ms"]):
+                t = o["ms"] * 1e-3
+                rt = max(o["flops"] / (peak * 1e12), o["bytes"] / (PEAK_HBM_GBS * 1e9))
+                f.write(f"{cls:12s} {name[:42]:42s} {o['n']:3d} {o['ms'] / a.profile_steps:8.3f} "
+                        f"{o['flops'] / t / 1e12:8.1f} {o['bytes'] / t / 1e9:8.1f} {100 * rt / t:6.1f}\n")
 
     if rank == 0:
         frames = a.batch * world * a.steps

@@ -16,8 +16,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdvie.so"
 DVIE_OK = 0
 DVIE_EINVAL = 1001
 F32, BF16 = 0, 1
-ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU = 0, 1, 2, 3
-EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW = range(8)
+ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3, 4
+EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW, EW_MASK = range(9)
 LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC = range(6)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
 OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD = 8, 9, 10, 11
@@ -90,7 +90,7 @@ class EwDesc(ctypes.Structure):
         ("c", i32), ("nsrc", i32), ("sh0", i32), ("sw0", i32),
         ("sh1", i32), ("sw1", i32), ("sh2", i32), ("sw2", i32),
         ("act", i32), ("dact", i32), ("beta", i32), ("dtype", i32),
-        ("ext_c", i32), ("pad0", i32),
+        ("ext_c", i32), ("align", i32),
         ("alpha", f32), ("scale", f32),
     ]
 
@@ -120,7 +120,7 @@ class BnDesc(ctypes.Structure):
         ("running_mean", vp), ("running_var", vp), ("partial", vp), ("stats", vp),
         ("x_ld", i64), ("y_ld", i64), ("g_ld", i64), ("dx_ld", i64), ("rows", i64),
         ("c", i32), ("splits", i32), ("act", i32), ("training", i32),
-        ("dtype", i32), ("accumulate", i32), ("beta_dx", i32), ("pad0", i32),
+        ("dtype", i32), ("accumulate", i32), ("beta_dx", i32), ("x_f32", i32),
         ("alpha", f32), ("eps", f32), ("momentum", f32), ("pad1", f32),
     ]
 

@@ -73,6 +73,7 @@ __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
     case DVIE_ACT_LRELU: return v > 0.f ? v : v * alpha;
     case DVIE_ACT_ELU: return v > 0.f ? v : expm1f(v);
     case DVIE_ACT_RELU: return v > 0.f ? v : 0.f;
+    case DVIE_ACT_TANH: return tanhf(v);
     default: return v;
   }
 }
@@ -83,6 +84,7 @@ __device__ __forceinline__ float act_dz(float z, int act, float alpha) {
     case DVIE_ACT_LRELU: return z > 0.f ? 1.f : alpha;
     case DVIE_ACT_ELU: return z > 0.f ? 1.f : z + 1.f;
     case DVIE_ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case DVIE_ACT_TANH: return 1.f - z * z;
     default: return 1.f;
   }
 }

@@ -38,6 +38,8 @@ __device__ __forceinline__ void act1(float* v, int act, float alpha) {
     for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
   } else if (act == DVIE_ACT_ELU) {
     for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : expm1f(v[k]);
+  } else if (act == DVIE_ACT_TANH) {
+    for (int k = 0; k < 8; ++k) v[k] = tanhf(v[k]);
   }
 }
 
@@ -48,6 +50,8 @@ __device__ __forceinline__ void dact1(float* v, const float* z, int dact, float 
     for (int k = 0; k < 8; ++k) v[k] = z[k] > 0.f ? v[k] : 0.f;
   } else if (dact == DVIE_ACT_ELU) {
     for (int k = 0; k < 8; ++k) v[k] *= z[k] > 0.f ? 1.f : z[k] + 1.f;
+  } else if (dact == DVIE_ACT_TANH) {
+    for (int k = 0; k < 8; ++k) v[k] *= 1.f - z[k] * z[k];
   }
 }
 

@@ -57,6 +57,8 @@ __device__ __forceinline__ void act_apply(float* v, int n, int act, float alpha)
     for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
   } else if (act == DVIE_ACT_ELU) {
     for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : expm1f(v[k]);
+  } else if (act == DVIE_ACT_TANH) {
+    for (int k = 0; k < n; ++k) v[k] = tanhf(v[k]);
   }
 }
 
@@ -67,6 +69,8 @@ __device__ __forceinline__ void dact_apply(float* v, const float* z, int n, int 
     for (int k = 0; k < n; ++k) v[k] = z[k] > 0.f ? v[k] : 0.f;
   } else if (dact == DVIE_ACT_ELU) {
     for (int k = 0; k < n; ++k) v[k] *= z[k] > 0.f ? 1.f : z[k] + 1.f;
+  } else if (dact == DVIE_ACT_TANH) {
+    for (int k = 0; k < n; ++k) v[k] *= 1.f - z[k] * z[k];
   }
 }
 

@@ -1,5 +1,5 @@
 // NHWC pointwise kernels: multi-resolution fuse sums with bilinear upsampling
-// (align_corners=False), the gather-form adjoint of that upsampling, 2x2 average pooling
+// (align_corners False or True), the gather-form adjoint of that upsampling, 2x2 average pooling
 // and its adjoint, copies, feature-L1 sign gradients and NCHW<->NHWC packing.  Every op
 // shares the same epilogue (residual add, accumulate, activation, activation-derivative)
 // so backward contributions fuse into one pass.  Each thread owns 8 (bf16, 16-byte
@@ -13,15 +13,21 @@
 
 namespace dvie {
 
-// torch area_pixel_compute_source_index (align_corners=False, non-cubic) + the
-// neighbour/lambda selection of upsample_bilinear2d
+// torch area_pixel_compute_source_index (non-cubic) + the neighbour/lambda selection of
+// upsample_bilinear2d; align_corners=True maps the corner pixels onto each other
 struct Lerp {
   int i0, i1;
   float l0, l1;
 };
-__device__ __forceinline__ Lerp lerp_src(int dst, int in_size, int out_size) {
-  const float scale = (float)in_size / (float)out_size;
-  float src = scale * ((float)dst + 0.5f) - 0.5f;
+__device__ __forceinline__ Lerp lerp_src(int dst, int in_size, int out_size, int align) {
+  float src;
+  if (align) {
+    const float scale = out_size > 1 ? (float)(in_size - 1) / (float)(out_size - 1) : 0.f;
+    src = scale * (float)dst;
+  } else {
+    const float scale = (float)in_size / (float)out_size;
+    src = scale * ((float)dst + 0.5f) - 0.5f;
+  }
   if (src < 0.f) src = 0.f;
   Lerp r;
   r.i0 = (int)src;
@@ -66,7 +72,7 @@ struct VecN<T, 4> {
 
 template <typename T, int VW>
 __device__ __forceinline__ void up_sample_add(float* v, const T* __restrict__ s, long long ld, int n, int y, int x,
-                                              int c, int sh, int sw, int h, int w) {
+                                              int c, int sh, int sw, int h, int w, int align) {
   float t[VW];
   if (sh == h && sw == w) {
     VecN<T, VW>::load(s + (((long long)n * sh + y) * sw + x) * ld + c, t);
@@ -74,7 +80,7 @@ __device__ __forceinline__ void up_sample_add(float* v, const T* __restrict__ s,
     for (int k = 0; k < VW; ++k) v[k] += t[k];
     return;
   }
-  const Lerp ly = lerp_src(y, sh, h), lx = lerp_src(x, sw, w);
+  const Lerp ly = lerp_src(y, sh, h, align), lx = lerp_src(x, sw, w, align);
   const long long r0 = ((long long)n * sh + ly.i0) * sw, r1 = ((long long)n * sh + ly.i1) * sw;
   float a[VW], b[VW], cc[VW], d[VW];
   VecN<T, VW>::load(s + (r0 + lx.i0) * ld + c, a);
@@ -86,8 +92,8 @@ __device__ __forceinline__ void up_sample_add(float* v, const T* __restrict__ s,
 }
 
 // weight of fine index `f` (fine size `fs`) onto coarse index `cidx` (coarse size `cs`)
-__device__ __forceinline__ float upt_weight(int f, int cidx, int cs, int fs) {
-  const Lerp l = lerp_src(f, cs, fs);
+__device__ __forceinline__ float upt_weight(int f, int cidx, int cs, int fs, int align) {
+  const Lerp l = lerp_src(f, cs, fs, align);
   float wgt = 0.f;
   if (l.i0 == cidx) wgt += l.l0;
   if (l.i1 == cidx) wgt += l.l1;
@@ -110,28 +116,32 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
   for (int k = 0; k < VW; ++k) v[k] = 0.f;
   switch (p.op) {
     case DVIE_EW_FUSE:
-      up_sample_add<T, VW>(v, (const T*)p.src0, p.src_ld0, n, y, x, c, p.sh0, p.sw0, p.h, p.w);
-      if (p.nsrc > 1) up_sample_add<T, VW>(v, (const T*)p.src1, p.src_ld1, n, y, x, c, p.sh1, p.sw1, p.h, p.w);
-      if (p.nsrc > 2) up_sample_add<T, VW>(v, (const T*)p.src2, p.src_ld2, n, y, x, c, p.sh2, p.sw2, p.h, p.w);
+      up_sample_add<T, VW>(v, (const T*)p.src0, p.src_ld0, n, y, x, c, p.sh0, p.sw0, p.h, p.w, p.align);
+      if (p.nsrc > 1)
+        up_sample_add<T, VW>(v, (const T*)p.src1, p.src_ld1, n, y, x, c, p.sh1, p.sw1, p.h, p.w, p.align);
+      if (p.nsrc > 2)
+        up_sample_add<T, VW>(v, (const T*)p.src2, p.src_ld2, n, y, x, c, p.sh2, p.sw2, p.h, p.w, p.align);
       break;
     case DVIE_EW_UPT: {
       // coarse output (y, x) of a (h, w) grid, fine source (sh0, sw0)
       const T* s = (const T*)p.src0;
-      const float fy = (float)p.sh0 / (float)p.h, fx = (float)p.sw0 / (float)p.w;
-      int ylo = (int)floorf(((float)y - 0.5f) * fy - 0.5f) - 1, yhi = (int)ceilf(((float)y + 1.5f) * fy) + 1;
-      int xlo = (int)floorf(((float)x - 0.5f) * fx - 0.5f) - 1, xhi = (int)ceilf(((float)x + 1.5f) * fx) + 1;
+      // fine rows/cols whose bilinear stencil can touch coarse (y, x), widened by one
+      const float fy = p.align ? (float)(p.sh0 - 1) / (float)max(p.h - 1, 1) : (float)p.sh0 / (float)p.h;
+      const float fx = p.align ? (float)(p.sw0 - 1) / (float)max(p.w - 1, 1) : (float)p.sw0 / (float)p.w;
+      int ylo = (int)floorf(((float)y - 1.f) * fy - 0.5f) - 1, yhi = (int)ceilf(((float)y + 1.5f) * fy) + 1;
+      int xlo = (int)floorf(((float)x - 1.f) * fx - 0.5f) - 1, xhi = (int)ceilf(((float)x + 1.5f) * fx) + 1;
       if (ylo < 0) ylo = 0;
       if (xlo < 0) xlo = 0;
       if (yhi > p.sh0 - 1) yhi = p.sh0 - 1;
       if (xhi > p.sw0 - 1) xhi = p.sw0 - 1;
       for (int Y = ylo; Y <= yhi; ++Y) {
-        const float wy = upt_weight(Y, y, p.h, p.sh0);
+        const float wy = upt_weight(Y, y, p.h, p.sh0, p.align);
         if (wy == 0.f) continue;
         float rowv[VW];
 #pragma unroll
         for (int k = 0; k < VW; ++k) rowv[k] = 0.f;
         for (int X = xlo; X <= xhi; ++X) {
-          const float wx = upt_weight(X, x, p.w, p.sw0);
+          const float wx = upt_weight(X, x, p.w, p.sw0, p.align);
           if (wx == 0.f) continue;
           float t[VW];
           VecN<T, VW>::load(s + (((long long)n * p.sh0 + Y) * p.sw0 + X) * p.src_ld0 + c, t);
@@ -189,6 +199,14 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
       }
       break;
     }
+    case DVIE_EW_MASK: {
+      const float m = p.ext[(long long)n * p.sn + (long long)y * p.sh + (long long)x * p.sw];
+      const float f = p.ext_c ? 1.f - m : m;
+      VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, v);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] *= f;
+      break;
+    }
     case DVIE_EW_TONCHW: {
       float a[VW];
       VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, a);
@@ -240,7 +258,8 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
   DVIE_CHECK_ARG(d->op == DVIE_EW_TONCHW || (d->y && d->y_ld % 4 == 0), "ew: y");
   if (d->op == DVIE_EW_POOL) DVIE_CHECK_ARG(d->sh0 == 2 * d->h && d->sw0 == 2 * d->w, "ew: pool shape");
   if (d->op == DVIE_EW_POOLT) DVIE_CHECK_ARG(d->h == 2 * d->sh0 && d->w == 2 * d->sw0, "ew: poolT shape");
-  if (d->op == DVIE_EW_NCHW || d->op == DVIE_EW_TONCHW) DVIE_CHECK_ARG(d->ext != nullptr, "ew: ext");
+  if (d->op == DVIE_EW_NCHW || d->op == DVIE_EW_TONCHW || d->op == DVIE_EW_MASK)
+    DVIE_CHECK_ARG(d->ext != nullptr, "ew: ext");
   if (d->dact) DVIE_CHECK_ARG(d->z != nullptr && d->z_ld % 4 == 0, "ew: z");
   DVIE_CHECK_ARG((long long)d->n * d->h < 65536 && (long long)d->w * d->c < (1LL << 30), "ew: grid too large");
   hipStream_t s = (hipStream_t)stream;

@@ -16,9 +16,9 @@ constexpr int BN_THREADS = 256;
 
 // mode 0: s1 += x, s2 += x^2                  (forward statistics)
 // mode 1: s1 += g, s2 += g * (x - mean[c])     (backward statistics; a = g, b = x)
-template <typename T>
-__global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const T* __restrict__ a, long long a_ld,
-                                                              const T* __restrict__ b, long long b_ld,
+template <typename TA, typename TB>
+__global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const TA* __restrict__ a, long long a_ld,
+                                                              const TB* __restrict__ b, long long b_ld,
                                                               const float* __restrict__ mean, long long rows, int c,
                                                               long long rows_per_split, double* __restrict__ part,
                                                               int mode) {
@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const T* __restric
     f32x4 mu = {0.f, 0.f, 0.f, 0.f};
     if (mode == 1) mu = *(const f32x4*)(mean + 4 * g);
     for (long long r = r0 + rl; r < r1; r += lanes) {
-      const f32x4 va = V4<T>::load(a + r * a_ld + 4 * g);
+      const f32x4 va = V4<TA>::load(a + r * a_ld + 4 * g);
       if (mode == 0) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(const T* __restric
           s2[k] += (double)va[k] * (double)va[k];
         }
       } else {
-        const f32x4 vb = V4<T>::load(b + r * b_ld + 4 * g);
+        const f32x4 vb = V4<TB>::load(b + r * b_ld + 4 * g);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           s1[k] += (double)va[k];
@@ -137,7 +137,7 @@ __global__ void bn_fold_bwd_kernel(dvie_bn_desc d) {
 }
 
 // forward: y = act(x*scale + shift); backward (bwd=1): dx (+)= A*(g - mg) + B*(x - mean)
-template <typename T>
+template <typename TX, typename T>
 __global__ void bn_apply_kernel(dvie_bn_desc d, int bwd) {
   const int cg = d.c >> 2;
   const long long total = d.rows * cg;
@@ -146,7 +146,7 @@ __global__ void bn_apply_kernel(dvie_bn_desc d, int bwd) {
        i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / cg;
     const int ch = (int)(i - r * cg) * 4;
-    const f32x4 xv = V4<T>::load((const T*)d.x + r * d.x_ld + ch);
+    const f32x4 xv = V4<TX>::load((const TX*)d.x + r * d.x_ld + ch);
     f32x4 o;
     if (!bwd) {
       const f32x4 sc = *(const f32x4*)(d.stats + 2 * c + ch);
@@ -312,6 +312,37 @@ static int bn_check(const dvie_bn_desc* d) {
   return DVIE_OK;
 }
 
+// x (the BatchNorm input, a conv output) may be fp32 while y / g / dx have the compute
+// dtype: bf16 storage of a pre-normalisation tensor whose |mean| >> std would cost
+// 2^-9 * |mean| / std relative precision in x - mean.
+template <typename TX, typename T>
+static void bn_launch(const dvie_bn_desc* d, hipStream_t st, int bwd) {
+  const long long rps = (d->rows + d->splits - 1) / d->splits;
+  if (!bwd) {
+    if (d->training)
+      hipLaunchKernelGGL((bn_stats_kernel<TX, TX>), dim3(d->splits), dim3(BN_THREADS), 0, st, (const TX*)d->x,
+                         d->x_ld, (const TX*)nullptr, 0LL, (const float*)nullptr, d->rows, d->c, rps, d->partial, 0);
+    hipLaunchKernelGGL(bn_fold_fwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
+  } else {
+    hipLaunchKernelGGL((bn_stats_kernel<T, TX>), dim3(d->splits), dim3(BN_THREADS), 0, st, (const T*)d->g, d->g_ld,
+                       (const TX*)d->x, d->x_ld, (const float*)d->stats, d->rows, d->c, rps, d->partial, 1);
+    hipLaunchKernelGGL(bn_fold_bwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
+  }
+  const long long n4 = d->rows * (d->c / 4);
+  hipLaunchKernelGGL((bn_apply_kernel<TX, T>), dim3(grid_1d(n4)), dim3(256), 0, st, *d, bwd);
+}
+
+static void bn_dispatch(const dvie_bn_desc* d, hipStream_t st, int bwd) {
+  if (d->dtype == DVIE_BF16) {
+    if (d->x_f32)
+      bn_launch<float, bf16_t>(d, st, bwd);
+    else
+      bn_launch<bf16_t, bf16_t>(d, st, bwd);
+  } else {
+    bn_launch<float, float>(d, st, bwd);
+  }
+}
+
 }  // namespace dvie
 
 using namespace dvie;
@@ -330,27 +361,11 @@ int dvie_bn_fwd(const dvie_bn_desc* d, void* stream) {
   int rc = bn_check(d);
   if (rc) return rc;
   DVIE_CHECK_ARG(d->y && d->y_ld % 4 == 0, "bn fwd: y");
-  hipStream_t st = (hipStream_t)stream;
-  if (d->training) {
+  if (d->training)
     DVIE_CHECK_ARG(d->partial && d->splits >= 1, "bn fwd: partial workspace");
-    const long long rps = (d->rows + d->splits - 1) / d->splits;
-    if (d->dtype == DVIE_BF16)
-      hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(d->splits), dim3(BN_THREADS), 0, st, (const bf16_t*)d->x,
-                         d->x_ld, (const bf16_t*)nullptr, 0LL, (const float*)nullptr, d->rows, d->c, rps, d->partial,
-                         0);
-    else
-      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(d->splits), dim3(BN_THREADS), 0, st, (const float*)d->x,
-                         d->x_ld, (const float*)nullptr, 0LL, (const float*)nullptr, d->rows, d->c, rps, d->partial,
-                         0);
-  } else {
-    DVIE_CHECK_ARG(d->running_mean && d->running_var, "bn eval: running statistics");
-  }
-  hipLaunchKernelGGL(bn_fold_fwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
-  const long long n4 = d->rows * (d->c / 4);
-  if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(grid_1d(n4)), dim3(256), 0, st, *d, 0);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_1d(n4)), dim3(256), 0, st, *d, 0);
+    DVIE_CHECK_ARG(d->running_mean && d->running_var, "bn eval: running statistics");
+  bn_dispatch(d, (hipStream_t)stream, 0);
   DVIE_RETURN_LAUNCH();
 }
 
@@ -360,22 +375,7 @@ int dvie_bn_bwd(const dvie_bn_desc* d, void* stream) {
   DVIE_CHECK_ARG(d->training, "bn bwd: only training-mode statistics have a backward here");
   DVIE_CHECK_ARG(d->g && d->dx && d->partial && d->splits >= 1 && d->g_ld % 4 == 0 && d->dx_ld % 4 == 0,
                  "bn bwd: args");
-  hipStream_t st = (hipStream_t)stream;
-  const long long rps = (d->rows + d->splits - 1) / d->splits;
-  if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, dim3(d->splits), dim3(BN_THREADS), 0, st, (const bf16_t*)d->g,
-                       d->g_ld, (const bf16_t*)d->x, d->x_ld, (const float*)d->stats, d->rows, d->c, rps, d->partial,
-                       1);
-  else
-    hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(d->splits), dim3(BN_THREADS), 0, st, (const float*)d->g,
-                       d->g_ld, (const float*)d->x, d->x_ld, (const float*)d->stats, d->rows, d->c, rps, d->partial,
-                       1);
-  hipLaunchKernelGGL(bn_fold_bwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
-  const long long n4 = d->rows * (d->c / 4);
-  if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(grid_1d(n4)), dim3(256), 0, st, *d, 1);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_1d(n4)), dim3(256), 0, st, *d, 1);
+  bn_dispatch(d, (hipStream_t)stream, 1);
   DVIE_RETURN_LAUNCH();
 }
 

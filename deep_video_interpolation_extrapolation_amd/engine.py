@@ -159,8 +159,8 @@ class ConvOp(_Op):
 
 
 class FuseOp(_Op):
-    def __init__(self, srcs, out, act):
-        self.srcs, self.out, self.act = srcs, out, act
+    def __init__(self, srcs, out, act, align=False):
+        self.srcs, self.out, self.act, self.align = srcs, out, act, align
 
     def inputs(self):
         return list(self.srcs)
@@ -205,6 +205,28 @@ class BNOp(_Op):
 
     def inputs(self):
         return [self.x]
+
+
+class MaskOp(_Op):
+    """out = src * m (or src * (1 - m)), m = channel `chan` of an external NCHW fp32 mask
+    (the fg/bg split of nets/SepUNet.py:45-46).  The mask is data: no gradient to it."""
+
+    def __init__(self, src, out, key, chan, inverse):
+        self.src, self.out, self.key, self.chan, self.inverse, self.act = src, out, key, chan, inverse, L.ACT_NONE
+
+    def inputs(self):
+        return [self.src]
+
+
+class OutNCHWOp(_Op):
+    """Sink: copy an internal region to an external NCHW fp32 tensor (outputs whose
+    producer carries an activation, e.g. the tanh RGB head of UNet/SepUNet)."""
+
+    def __init__(self, region, key, channels):
+        self.region, self.key, self.channels, self.out, self.act = region, key, channels, None, L.ACT_NONE
+
+    def inputs(self):
+        return []
 
 
 class HeadOp(_Op):
@@ -262,12 +284,21 @@ class Graph:
         self._add(ConvOp(x, lay, out, act, res))
         return out
 
-    def fuse(self, srcs, out, act=L.ACT_NONE):
+    def fuse(self, srcs, out, act=L.ACT_NONE, align=False):
         assert 1 <= len(srcs) <= 3
         for s in srcs:
             assert s.c == out.c
-        self._add(FuseOp(srcs, out, act))
+        self._add(FuseOp(srcs, out, act, align))
         return out
+
+    def mask(self, src, out, key, chan, inverse=False):
+        assert (src.H, src.W, src.c) == (out.H, out.W, out.c)
+        self._add(MaskOp(src, out, key, chan, inverse))
+        return out
+
+    def output_nchw(self, key, region, channels):
+        self._add(OutNCHWOp(region, key, channels))
+        self.outputs[key] = (region, channels)
 
     def pool(self, x, out):
         assert (out.H * 2, out.W * 2, out.c) == (x.H, x.W, x.c)
@@ -275,7 +306,10 @@ class Graph:
         return out
 
     def bn(self, x, module, out, act=L.ACT_NONE, trainable=True):
+        """x: a conv output buffer read only by this op; it is kept in fp32 whatever the
+        compute dtype (x - mean loses 2^-9 * |mean| / std relative precision in bf16)."""
         assert (x.H, x.W, x.c) == (out.H, out.W, out.c) and x.c == rup(module.num_features, PADC)
+        x.buf.dtype = torch.float32
         self._add(BNOp(x, module, out, act, trainable))
         return out
 
@@ -529,8 +563,24 @@ class Plan:
             elif isinstance(op, FuseOp):
                 out = op.out
                 srcs = [(self.ptr(s), s.buf.C, s.H, s.W) for s in op.srcs]
-                self.fwd.append(self.ew_desc(L.EW_FUSE, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C, srcs,
-                                             act=op.act))
+                o = self.ew_desc(L.EW_FUSE, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C, srcs, act=op.act)
+                o.u.ew.align = int(op.align)
+                self.fwd.append(o)
+            elif isinstance(op, MaskOp):
+                out, src = op.out, op.src
+                o = self.ew_desc(L.EW_MASK, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C,
+                                 [(self.ptr(src), src.buf.C, src.H, src.W)])
+                o.u.ew.ext_c = int(op.inverse)
+                self.ext_mask = getattr(self, "ext_mask", {})
+                self.ext_mask.setdefault(op.key, []).append(("fwd", len(self.fwd), op))
+                self.fwd.append(o)
+            elif isinstance(op, OutNCHWOp):
+                r = op.region
+                o = self.ew_desc(L.EW_TONCHW, nf, r.H, r.W, r.c, 0, 0, [(self.ptr(r), r.buf.C, r.H, r.W)])
+                o.u.ew.ext_c = op.channels
+                self.ext_nchw_out = getattr(self, "ext_nchw_out", {})
+                self.ext_nchw_out[op.key] = len(self.fwd)
+                self.fwd.append(o)
             elif isinstance(op, PoolOp):
                 x, out = op.x, op.out
                 self.fwd.append(self.ew_desc(L.EW_POOL, nf, out.H, out.W, out.c, self.ptr(out), out.buf.C,
@@ -589,6 +639,7 @@ class Plan:
         assert m.num_features == x.c, "BatchNorm channel count must be a multiple of 8"
         d.training = int(getattr(self.g, "bn_training", True))
         d.act, d.alpha, d.eps = op.act, 0.2, m.eps
+        d.x_f32 = int(x.buf.dt == torch.float32 and self.dtype != torch.float32)
         d.momentum = m.momentum if m.momentum is not None else 0.0
         d.dtype = self.dt
 
@@ -661,14 +712,17 @@ class Plan:
                 self._uses_left[op.layer] = self._uses_left.get(op.layer, 0) + 1
         for key, (region, ch) in g.outputs.items():
             b = region.buf
-            assert b.needs_grad and b.expected == 0 and all(p.act == L.ACT_NONE for p in b.producers)
+            assert b.needs_grad and b.expected == 0
+            assert b.t is not None or all(p.act == L.ACT_NONE for p in b.producers), "external output with activation"
             o = self.ew_desc(L.EW_NCHW, nb, region.H, region.W, region.c, self.ptr(region, grad=True), b.C)
             o.u.ew.ext_c = ch
             self.ext_ograd[key] = len(self.bwd)
             self.bwd.append(o)
             b.done = True
-            b.dact_done = True
+            b.dact_done = all(p.act == L.ACT_NONE for p in b.producers)  # else _ensure_dact at the producer
         for op in reversed(g.ops):
+            if isinstance(op, OutNCHWOp):
+                continue
             if isinstance(op, HeadOp):
                 x = op.x
                 if not x.buf.needs_grad:
@@ -746,11 +800,27 @@ class Plan:
                     else:
                         sp = self.ptr(s, grad=True)
 
-                        def em(beta, res, res_ld, dact, z, z_ld, s=s, sp=sp, out=out, gout=gout, gld=gld):
-                            return [self.ew_desc(L.EW_UPT, nb, s.H, s.W, s.c, sp, s.buf.C, [(gout, gld, out.H, out.W)],
-                                                 res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)]
+                        def em(beta, res, res_ld, dact, z, z_ld, s=s, sp=sp, out=out, gout=gout, gld=gld, op=op):
+                            o = self.ew_desc(L.EW_UPT, nb, s.H, s.W, s.c, sp, s.buf.C, [(gout, gld, out.H, out.W)],
+                                             res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)
+                            o.u.ew.align = int(op.align)
+                            return [o]
 
                         self._contrib(s, em)
+            elif isinstance(op, MaskOp):
+                src = op.src
+                if src.buf.needs_grad:
+                    sp = self.ptr(src, grad=True)
+
+                    def em(beta, res, res_ld, dact, z, z_ld, src=src, sp=sp, out=out, gout=gout, gld=gld, op=op):
+                        o = self.ew_desc(L.EW_MASK, nb, src.H, src.W, src.c, sp, src.buf.C, [(gout, gld, out.H, out.W)],
+                                         res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)
+                        o.u.ew.ext_c = int(op.inverse)
+                        self.ext_mask = getattr(self, "ext_mask", {})
+                        self.ext_mask.setdefault(op.key, []).append(("bwd", len(self.bwd), op))
+                        return [o]
+
+                    self._contrib(src, em)
             elif isinstance(op, PoolOp):
                 x = op.x
                 if x.buf.needs_grad:
@@ -862,6 +932,12 @@ class Plan:
                 o.u.wreduce.ws = self.ws.data_ptr()
         # pack op (all layers, one launch) goes first in the forward list
         descs = self._pack_descs
+        if not descs:  # no convolutions (e.g. a pointwise-only plan)
+            self.fwd_arr = (L.Op * max(1, len(self.fwd)))(*self.fwd)
+            self.fwd_off = 0
+            self.bwd_arr = (L.Op * max(1, len(self.bwd)))(*self.bwd) if self.bwd else None
+            self.n_bwd = len(self.bwd)
+            return
         arr = (L.PackDesc * len(descs))(*descs)
         raw = bytes(arr)
         dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
@@ -892,6 +968,23 @@ class Plan:
             d = self.fwd_arr[idx + self.fwd_off].u.conv
             d.y = t.data_ptr() + region.c0 * t.element_size()
             d.y_ld = t.shape[-1]
+
+    def set_mask(self, key, t):
+        """Patch the external NCHW fp32 mask `key` (channel op.chan of t) into its ops."""
+        assert t.dtype == torch.float32 and t.device.type == self.device.type
+        sn, sc, sh, sw = t.stride()
+        for where, idx, op in getattr(self, "ext_mask", {}).get(key, []):
+            d = (self.fwd_arr[idx + self.fwd_off] if where == "fwd" else self.bwd_arr[idx]).u.ew
+            d.ext = t.data_ptr() + 4 * op.chan * sc
+            d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+
+    def set_output_nchw(self, key, t):
+        """Point the NCHW sink `key` at an fp32 tensor (any strides)."""
+        assert t.dtype == torch.float32
+        d = self.fwd_arr[self.ext_nchw_out[key] + self.fwd_off].u.ew
+        sn, sc, sh, sw = t.stride()
+        d.ext = t.data_ptr()
+        d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
 
     def set_head_output(self, key, t):
         """Point head `key` at an fp32 vector of length n*(h/pool)*(w/pool)."""
@@ -943,6 +1036,16 @@ class Plan:
             if first:
                 d.beta = int(accumulate)
 
+    def activation_signs(self):
+        """{buffer name: bool NCHW CPU tensor (value > 0)} for every buffer written by a
+        LeakyReLU-activated op in the last forward (test support: which branch each
+        activation took, so an fp64 oracle can be evaluated on the same branches)."""
+        out = {}
+        for b in self.g.buffers:
+            if b.t is not None and b.producers and all(p.act == L.ACT_LRELU for p in b.producers):
+                out[b.name] = (b.t > 0).permute(0, 3, 1, 2).cpu()
+        return out
+
     def _nonfinite(self):
         """names of buffers (activations / gradients) holding non-finite values (debug)."""
         out = set()
@@ -979,7 +1082,7 @@ class Plan:
 
     def run_forward(self, stream=None):
         s = L.stream_ptr() if stream is None else stream
-        metas = [None] + [getattr(o, "meta", None) for o in self.fwd]
+        metas = [None] * self.fwd_off + [getattr(o, "meta", None) for o in self.fwd]
         self._run(self.fwd_arr, 0, len(self.fwd_arr), s, "forward plan", metas)
         self.generation += 1
 

@@ -6,3 +6,4 @@ from .InterNet import InterNet
 from .vgg import VGG19, my_vgg, vgg19_features
 from .disc import FrameDiscriminator, ResnetBlock, VideoDiscriminator
 from .InterGANNet import InterGANNet, channel_softmax
+from .UNet import SegEncoder, SepUNet, UNet, double_conv, down, inconv, outconv, up

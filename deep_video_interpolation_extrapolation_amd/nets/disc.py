@@ -140,10 +140,10 @@ class _PlanDiscriminator(FlatParams, nn.Module):
         plan.set_head_output("score", out)
         plan.run_forward()
         self.last_plan = plan
-        if self.training:
-            for m in self.modules():
-                if isinstance(m, nn.BatchNorm2d) and m.num_batches_tracked is not None:
-                    m.num_batches_tracked.add_(1)
+        if self.training:  # one increment per BatchNorm call, as nn.BatchNorm2d.train()
+            for op in plan.g.ops:
+                if isinstance(op, E.BNOp) and op.m.num_batches_tracked is not None:
+                    op.m.num_batches_tracked.add_(1)
         return plan, (out,)
 
     def run_backward(self, plan, inputs, grads, needs):
@@ -163,13 +163,8 @@ class _PlanDiscriminator(FlatParams, nn.Module):
         return outs
 
     def activation_signs(self):
-        """{buffer name: bool NCHW tensor (value > 0)} of the last forward's LeakyReLU
-        outputs (test support: the branch each activation took)."""
-        out = {}
-        for b in self.last_plan.g.buffers:
-            if b.t is not None and (b.name.startswith("layer.") and not b.name.endswith(".out")):
-                out[b.name] = (b.t > 0).permute(0, 3, 1, 2).cpu()
-        return out
+        """branch taken by every LeakyReLU of the last forward (see Plan.activation_signs)"""
+        return self.last_plan.activation_signs()
 
     def _run(self, *inputs):
         ins = [t.float() for t in inputs]

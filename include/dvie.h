@@ -38,6 +38,7 @@ extern "C" {
 #define DVIE_ACT_LRELU 1 /* nn.LeakyReLU(0.2)  nets/HRNet.py:22,59,107 */
 #define DVIE_ACT_ELU 2   /* nn.ELU()           nets/HRNet.py:360,362    */
 #define DVIE_ACT_RELU 3  /* VGG19 ReLU         nets/vgg.py:11-54         */
+#define DVIE_ACT_TANH 4  /* F.tanh RGB head    nets/UNet.py:151, nets/SepUNet.py:65 (tanh'(z) = 1 - z^2) */
 
 /*
  * Implicit-GEMM convolution (forward, and data-gradient as a forward conv over the
@@ -166,10 +167,12 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
  * Pointwise NHWC family (4 channels per thread).  op selects:
  *  DVIE_EW_FUSE   y = act( sum_i up_i(src_i) ) — HighResolutionModule fuse sum
  *                 (nets/HRNet.py:212-225) and the final bilinear upsample into the
- *                 448-channel concat (nets/HRNet.py:576-582).  up_i is bilinear,
- *                 align_corners=False, from (src_h, src_w) to (h, w), identity when equal.
+ *                 448-channel concat (nets/HRNet.py:576-582).  up_i is bilinear from
+ *                 (src_h, src_w) to (h, w), identity when equal; align_corners=False, or
+ *                 True when `align` is set (nn.Upsample of nets/UNet.py:70).
  *  DVIE_EW_UPT    y = up^T(src_0) — adjoint of the bilinear upsample (gather form,
- *                 deterministic, no atomics); src_0 is the fine grid (src_h x src_w).
+ *                 deterministic, no atomics); src_0 is the fine grid (src_h x src_w);
+ *                 `align` as for FUSE.
  *  DVIE_EW_POOL   y = avgpool2x2(src_0) (nets/vgg.py:9 AvgPool2d(2,2)).
  *  DVIE_EW_POOLT  y = adjoint of avgpool2x2 applied to src_0 (coarse grid).
  *  DVIE_EW_COPY   y = src_0 (same grid).
@@ -180,6 +183,9 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
  *  DVIE_EW_TONCHW ext (+)= channels [0, ext_c) of src_0 as fp32 with NCHW strides,
  *                 divided by std[c] when std is set (adjoint of the normalisation);
  *                 beta selects accumulate; the NHWC epilogue is not applied.
+ *  DVIE_EW_MASK   y = src_0 * m or src_0 * (1 - m) (ext_c = 0 / 1), m = ext[n, 0, y, x]
+ *                 (fp32, NCHW strides): the fg/bg split of nets/SepUNet.py:45-46 (its own
+ *                 adjoint with respect to src_0).
  * then the shared epilogue: v += res; v += y_old (beta); v = act(v); v *= act'(z); y = v.
  * Channels c % 4 == 0; all lds % 4 == 0.
  */
@@ -191,6 +197,7 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
 #define DVIE_EW_L1SIGN 5
 #define DVIE_EW_NCHW 6
 #define DVIE_EW_TONCHW 7
+#define DVIE_EW_MASK 8
 
 typedef struct dvie_ew_desc {
   void* y;
@@ -208,7 +215,7 @@ typedef struct dvie_ew_desc {
   int c, nsrc, sh0, sw0;
   int sh1, sw1, sh2, sw2;
   int act, dact, beta, dtype;
-  int ext_c, pad0;
+  int ext_c, align;
   float alpha, scale;
 } dvie_ew_desc;
 
@@ -317,7 +324,7 @@ typedef struct dvie_bn_desc {
   long long x_ld, y_ld, g_ld, dx_ld;
   long long rows;
   int c, splits, act, training;
-  int dtype, accumulate, beta_dx, pad0;
+  int dtype, accumulate, beta_dx, x_f32; /* x_f32: x is fp32 (y, g, dx have elem type dtype) */
   float alpha, eps, momentum, pad1;
 } dvie_bn_desc;
 

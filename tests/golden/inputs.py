@@ -84,3 +84,14 @@ def disc_inputs(n=2, H=128, W=256, seed=21):
 def sample_idx(numel, k=256, seed=99):
     """fixed sample positions for large-tensor fixtures"""
     return torch.randint(0, numel, (k,), generator=_gen(seed))
+
+
+def sepunet_inputs(n=2, H=32, W=64, seed=41):
+    """SepUNet input [frames 6 | segs 40], fg_mask (n, 2, H, W) in [0, 1], output grads."""
+    g = _gen(seed)
+    x = torch.rand((n, 6, H, W), generator=g) * 2 - 1
+    seg = torch.cat([onehot(torch.randint(0, 20, (n, H, W), generator=g)) for _ in range(2)], 1)
+    mask = (torch.rand((n, 2, H, W), generator=g) > 0.5).float() * 0.8 + 0.1
+    g_rgb = torch.randn((n, 3, H, W), generator=g)
+    g_seg = torch.randn((n, 20, H, W), generator=g)
+    return torch.cat([x, seg], 1), mask, g_rgb, g_seg

@@ -16,6 +16,9 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
                      in train mode) at 128x128 and 128x256 (NCHW-flat head grouping): scores,
                      input gradients, parameter-gradient stats, running statistics, hinge
                      losses, eval-mode scores
+  sepunet.npz    G7: reference SepUNet (train-mode BatchNorm, align_corners=True upsampling,
+                     tanh head) at 32x64: outputs, input-gradient stats, parameter-gradient
+                     stats, running statistics
   step.npz       G4: one training step of the reference modules (InterTrainer.py:380-441
                      body): loss dict, per-parameter gradient stats, post-Adamax checksums
 """
@@ -178,9 +181,31 @@ def g6():
     np.savez_compressed(os.path.join(HERE, "disc.npz"), **out)
 
 
+def g7():
+    torch.manual_seed(5)
+    m = ref_nets.SepUNet(args_ns())
+    m.train()
+    inp, mask, g_rgb, g_seg = inputs.sepunet_inputs()
+    inp = inp.clone().requires_grad_(True)
+    rgb, seg = m(inp, fg_mask=mask)
+    (rgb * g_rgb).sum().add((seg * g_seg).sum()).backward()
+    named = dict(m.named_parameters())
+    names = sorted(named)
+    gi = inp.grad.double().reshape(-1)
+    bufs = {k: v for k, v in m.state_dict().items() if "running" in k}
+    np.savez_compressed(os.path.join(HERE, "sepunet.npz"), rgb=rgb.detach().numpy(), seg=seg.detach().numpy(),
+                        gin=np.concatenate([[float(gi.sum()), float(gi.abs().sum()), float(gi.norm())],
+                                            gi[inputs.sample_idx(gi.numel())].numpy()]),
+                        param_names=np.array(names),
+                        grad_stats=np.array([[float(named[n].grad.double().sum()),
+                                              float((named[n].grad.double() ** 2).sum())] for n in names]),
+                        buf_names=np.array(sorted(bufs)),
+                        bufs=np.concatenate([bufs[k].numpy().reshape(-1) for k in sorted(bufs)]))
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()
