@@ -87,3 +87,20 @@ def test_plan_reuse_and_busy_guard(dev):
     (r1.sum() + r2.sum()).backward()
     n_plans = sum(len(v) for v in m.coarse_model._pool.plans.values())
     assert n_plans == 2
+
+
+def test_main_launcher_one_epoch(dev, tmp_path):
+    """The launcher (reference main.py flow): one training epoch on 2 synthetic clips, then
+    the rank-0 checkpoint, then a validation pass reloading that checkpoint."""
+    from deep_video_interpolation_extrapolation_amd import main as M
+    common = ["--syn_type", "inter", "--bs", "2", "--input_h", "32", "--input_w", "64", "--epochs", "1",
+              "--save_dir", str(tmp_path), "--synthetic", "2", "--nw", "0", "--precision", "fp32"]
+    M.main(common + ["INTER", "--train_coarse"])
+    runs = list(tmp_path.iterdir())
+    assert len(runs) == 1
+    ck = list((runs[0] / "checkpoint").iterdir())
+    assert len(ck) == 1 and ck[0].name.startswith("InterNet_xs2xs_inter_0_1_")
+    sd = torch.load(ck[0], map_location="cpu", weights_only=True)
+    assert set(sd) == {"session", "epoch", "coarse_model", "coarse_opt"}
+    M.main(common + ["--split", "val", "--load_dir", str(runs[0]), "--checkepoch", "1", "--checkpoint",
+                          ck[0].name.split("_")[-1][:-4], "--checksession", "0", "INTER", "--load_coarse"])
