@@ -143,6 +143,14 @@ class SoftmaxDesc(ctypes.Structure):
     ]
 
 
+class SnLayer(ctypes.Structure):
+    _fields_ = [
+        ("w_bar", vp), ("u", vp), ("v", vp), ("w_eff", vp), ("g_eff", vp), ("g_bar", vp), ("g_u", vp), ("g_v", vp),
+        ("state_off", i64),
+        ("h", i32), ("width", i32), ("power_iterations", i32), ("beta", i32),
+    ]
+
+
 class PackList(ctypes.Structure):
     _fields_ = [("descs_dev", vp), ("n", i32), ("max_elems", i32)]
 
@@ -160,14 +168,14 @@ class Op(ctypes.Structure):
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
-        100: WarpDesc, 101: SoftmaxDesc}
+        100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer}
 
 EXPORTS = [
     "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
     "dvie_ew", "dvie_loss", "dvie_loss_partial_count", "dvie_loss_ws_floats", "dvie_warp_fwd",
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
-    "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam",
+    "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd",
 ]
 
 _lib = None
@@ -216,6 +224,9 @@ def load():
         lib.dvie_adamax.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
         lib.dvie_scale.argtypes = [vp, i64, f32, vp]
         lib.dvie_adam.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
+        for name in ("dvie_sn_fwd", "dvie_sn_bwd"):
+            getattr(lib, name).argtypes = [vp, i32, vp, vp]
+            getattr(lib, name).restype = i32
         _lib = lib
         return lib
 

@@ -215,6 +215,7 @@ size_t dvie_abi_sizeof(int which) {
     case DVIE_OP_HEAD_FWD: return sizeof(dvie_head_desc);
     case 100: return sizeof(dvie_warp_desc);
     case 101: return sizeof(dvie_softmax_desc);
+    case 102: return sizeof(dvie_sn_layer);
     default: return 0;
   }
 }

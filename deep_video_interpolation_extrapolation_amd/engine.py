@@ -1014,8 +1014,10 @@ class Plan:
             d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
             d.beta = int(accumulate)
 
-    def set_param_grads(self, accumulate=False):
-        """Point weight reductions at the parameters' .grad tensors (fp32, OIHW)."""
+    def set_param_grads(self, accumulate=False, fresh=()):
+        """Point weight reductions at the parameters' .grad tensors (fp32, OIHW).  `fresh`:
+        ids of conv modules whose weight gradient this backward overwrites whatever
+        `accumulate` says (SpectralNorm's per-call d(W_bar / sigma) scratch)."""
         for idx, lay, which, first in self._grad_slots:
             if which == "bn":  # lay is the BatchNorm module: gamma and beta gradients
                 d = self.bwd_arr[idx].u.bn
@@ -1034,7 +1036,7 @@ class Plan:
             d = self.bwd_arr[idx].u.wreduce
             d.dw = p.grad.data_ptr()
             if first:
-                d.beta = int(accumulate)
+                d.beta = 0 if (which == "weight" and id(lay.m) in fresh) else int(accumulate)
 
     def activation_signs(self):
         """{buffer name: bool NCHW CPU tensor (value > 0)} for every buffer written by a

@@ -96,18 +96,16 @@ class InterGANNet(nn.Module):
         if self.video_disc:
             D_fake_video = self.video_disc_model(coarse_rgb.detach(), soft.detach(), input, seg, bboxes=bboxes)
             D_real_video = self.video_disc_model(gt_x, gt_seg, input, seg, bboxes=bboxes)
+        # G pass with the discriminator frozen, then set_net_grad(True) as in the reference
+        # (l.78-81, 93-97): every parameter is trainable afterwards, SpectralNorm u / v included
         if self.frame_disc:
-            saved = [p.requires_grad for p in self.frame_disc_model.parameters()]
             self.set_net_grad(self.frame_disc_model, False)
             G_fake_frame = self.frame_disc_model(coarse_rgb, soft, bboxes=bboxes)
-            for p, r in zip(self.frame_disc_model.parameters(), saved):
-                p.requires_grad = r
+            self.set_net_grad(self.frame_disc_model, True)
         if self.video_disc:
-            saved = [p.requires_grad for p in self.video_disc_model.parameters()]
             self.set_net_grad(self.video_disc_model, False)
             G_fake_video = self.video_disc_model(coarse_rgb, soft, input, seg, bboxes=bboxes)
-            for p, r in zip(self.video_disc_model.parameters(), saved):
-                p.requires_grad = r
+            self.set_net_grad(self.video_disc_model, True)
         return (coarse_rgb, coarse_seg, mu, var,
                 D_fake_frame, D_real_frame, D_fake_video, D_real_video, G_fake_frame, G_fake_video,
                 None, None, None, None, None, None, None, gen_bbox, loc_diff_loss)

@@ -4,6 +4,8 @@ from .ExtraNet import ExtraNet
 from .HRNet import HRNet
 from .InterNet import InterNet
 from .vgg import VGG19, my_vgg, vgg19_features
-from .disc import FrameDiscriminator, ResnetBlock, VideoDiscriminator
+from .disc import (FrameDiscriminator, FrameLocalDiscriminator, FrameSNDiscriminator, FrameSNLocalDiscriminator,
+                   ResnetBlock, ResnetSNBlock, SpectralNorm, VideoDiscriminator, VideoLocalDiscriminator,
+                   VideoSNDiscriminator, VideoSNLocalDiscriminator)
 from .InterGANNet import InterGANNet, channel_softmax
 from .UNet import SegEncoder, SepUNet, UNet, double_conv, down, inconv, outconv, up

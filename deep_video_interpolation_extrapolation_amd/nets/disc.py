@@ -1,18 +1,27 @@
 """Frame / video discriminators of InterGANNet on the MI355X plan engine.
 
 Module trees, construction order (so seeded initialisation) and state_dict keys are those
-of the reference: FrameDiscriminator nets/FrameDisc.py:35-75, VideoDiscriminator
-nets/VidDisc.py:34-84, ResnetBlock FrameDisc.py:8-19 / VidDisc.py:8-19.  The forward and
-backward do not run the submodules: `_lower` turns `self.layer` into one engine plan
-(HIP convs with fused bias / residual / LeakyReLU epilogues, BatchNorm with batch
-statistics fused with its LeakyReLU, and the AvgPool + view(-1, C).mean(1) head).
+of the reference:
+  FrameDiscriminator nets/FrameDisc.py:35-75, FrameLocalDiscriminator l.77-114,
+  FrameSNDiscriminator l.116-156, FrameSNLocalDiscriminator l.158-189,
+  VideoDiscriminator nets/VidDisc.py:34-84, VideoLocalDiscriminator l.86-138,
+  VideoSNDiscriminator l.140-183, VideoSNLocalDiscriminator l.185-226,
+  ResnetBlock / ResnetSNBlock FrameDisc.py:8-32, SpectralNorm nets/SpectralNorm.py:14-68.
+The forward and backward do not run the submodules: `_lower` turns `self.layer` into one
+engine plan (HIP convs with fused bias / residual / LeakyReLU epilogues, BatchNorm with batch
+statistics fused with its LeakyReLU, the AvgPool + view(-1, C).mean(1) head, or, for the
+local variants, the last conv writing the (B, 1, h, w) map).  SpectralNorm layers get their
+power iteration in one HIP launch before the plan packs the weights (dvie_sn_fwd) and their
+sigma adjoint in one launch after its backward (dvie_sn_bwd).
 
-Calling conventions follow the reference: FrameDiscriminator(x, seg, bboxes=None) and
-VideoDiscriminator(x, seg, input_x, input_seg, bboxes=None) -> (B*k,) scores, where k is
-the number of pooled cells (k = 1 at the reference's 128x128 training crops).  The input
-concat (`torch.cat` in the reference forward) is never materialised: each input is packed
-into its own channel slice of the first conv's input buffer.
+Calling conventions follow the reference: Frame*(x, seg, bboxes=None) and
+Video*(x, seg, input_x, input_seg, bboxes=None) -> (B*k,) scores (k pooled cells; k = 1 at
+the reference's 128x128 training crops) or the (B, 1, h, w) map of the local variants.  The
+input concat (`torch.cat` in the reference forward) is never materialised: each input is
+packed into its own channel slice of the first conv's input buffer.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -20,6 +29,44 @@ from .. import _lib as L
 from .. import engine as E
 from ..runtime import FlatParams, PlanFunction, PlanPool, precision_of
 from .conv import Conv2d
+
+
+def _l2normalize(v, eps=1e-12):
+    """SpectralNorm.py:10-11"""
+    return v / (v.norm() + eps)
+
+
+class SpectralNorm(nn.Module):
+    """Reference nets/SpectralNorm.py:14-68 (parameter holder).  The wrapped conv keeps the
+    reference's parameters `weight_u`, `weight_v` (requires_grad False), `weight_bar` and
+    `bias`, drawn in the reference's order, so state_dicts interchange.  `module.weight` is a
+    non-persistent buffer (a plain attribute in the reference, so not in the state_dict) that
+    receives W_bar / sigma from the owning discriminator's SpectralNorm launch before every
+    forward; the conv kernels pack it like any other weight."""
+
+    def __init__(self, module, name="weight", power_iterations=1):
+        super().__init__()
+        if name != "weight":
+            raise NotImplementedError("SpectralNorm over a parameter other than `weight`")
+        self.module, self.name, self.power_iterations = module, name, power_iterations
+        w = module.weight
+        height = w.data.shape[0]
+        width = w.view(height, -1).data.shape[1]
+        u = nn.Parameter(w.data.new(height).normal_(0, 1), requires_grad=False)
+        v = nn.Parameter(w.data.new(width).normal_(0, 1), requires_grad=False)
+        u.data = _l2normalize(u.data)
+        v.data = _l2normalize(v.data)
+        w_bar = nn.Parameter(w.data)
+        del module._parameters[name]
+        module.register_parameter(name + "_u", u)
+        module.register_parameter(name + "_v", v)
+        module.register_parameter(name + "_bar", w_bar)
+        module.register_buffer(name, torch.zeros_like(w.data), persistent=False)
+        self.h, self.width = height, width
+
+
+def _conv_of(m):
+    return m.module if isinstance(m, SpectralNorm) else m
 
 
 class ResnetBlock(nn.Module):
@@ -30,6 +77,16 @@ class ResnetBlock(nn.Module):
         self.conv = nn.Sequential(Conv2d(in_dim, out_dim, ks, stride=1, padding=ks // 2),
                                   nn.LeakyReLU(0.2, inplace=True),
                                   Conv2d(out_dim, out_dim, ks, stride=1, padding=ks // 2))
+
+
+class ResnetSNBlock(nn.Module):
+    """ResnetBlock with SpectralNorm convs (FrameDisc.py:21-32, VidDisc.py:21-32)."""
+
+    def __init__(self, in_dim, out_dim, ks):
+        super().__init__()
+        self.conv = nn.Sequential(SpectralNorm(Conv2d(in_dim, out_dim, ks, stride=1, padding=ks // 2)),
+                                  nn.LeakyReLU(0.2, inplace=True),
+                                  SpectralNorm(Conv2d(out_dim, out_dim, ks, stride=1, padding=ks // 2)))
 
 
 def _packing(widths):
@@ -49,13 +106,15 @@ def _packing(widths):
 
 
 class _PlanDiscriminator(FlatParams, nn.Module):
-    """Shared plan lowering / autograd plumbing of the two discriminators."""
+    """Shared plan lowering / autograd plumbing of the discriminators."""
 
     in_keys = ()
+    local = False  # True: the last conv's (B, 1, h, w) map is the output (no AvgPool head)
 
     def _finish_init(self):
         self.dtype = precision_of(self.args)
         self._pool = PlanPool(self._build_plan)
+        self._sn = [m for m in self.modules() if isinstance(m, SpectralNorm)]
         self._flatten()
 
     def _in_widths(self):
@@ -73,29 +132,37 @@ class _PlanDiscriminator(FlatParams, nn.Module):
         i, first = 0, True
         while i < len(mods):
             m = mods[i]
-            if isinstance(m, nn.Conv2d):
+            if isinstance(m, (nn.Conv2d, SpectralNorm)):
+                conv = _conv_of(m)
                 nxt = mods[i + 1] if i + 1 < len(mods) else None
-                hh = (x.H + 2 * m.padding[0] - m.kernel_size[0]) // m.stride[0] + 1
-                ww = (x.W + 2 * m.padding[1] - m.kernel_size[1]) // m.stride[1] + 1
+                hh = (x.H + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+                ww = (x.W + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
                 cm = cmap if first else None
                 first = False
+                if nxt is None:  # local variants: the map is the output
+                    assert self.local
+                    o = g.buffer("score", hh, ww, E.rup(conv.out_channels, 8), dtype=torch.float32, external=True)
+                    g.conv(x, conv, E.R(o), cmap=cm, trainable=trainable, name=f"layer.{i}")
+                    g.output("score", E.R(o), conv.out_channels)
+                    i += 1
+                    continue
                 if isinstance(nxt, nn.BatchNorm2d):
                     act = A.ACT_LRELU if i + 2 < len(mods) and isinstance(mods[i + 2], nn.LeakyReLU) else A.ACT_NONE
-                    t = g.buffer(f"layer.{i}", hh, ww, E.rup(m.out_channels, 8))
-                    g.conv(x, m, E.R(t), cmap=cm, trainable=trainable, name=f"layer.{i}")
-                    o = g.buffer(f"layer.{i + 1}", hh, ww, E.rup(m.out_channels, 8))
+                    t = g.buffer(f"layer.{i}", hh, ww, E.rup(conv.out_channels, 8))
+                    g.conv(x, conv, E.R(t), cmap=cm, trainable=trainable, name=f"layer.{i}")
+                    o = g.buffer(f"layer.{i + 1}", hh, ww, E.rup(conv.out_channels, 8))
                     g.bn(E.R(t), nxt, E.R(o), act=act, trainable=trainable)
                     x = E.R(o)
                     i += 3 if act == A.ACT_LRELU else 2
                     continue
                 act = A.ACT_LRELU if isinstance(nxt, nn.LeakyReLU) else A.ACT_NONE
-                o = g.buffer(f"layer.{i}", hh, ww, E.rup(m.out_channels, 8))
-                g.conv(x, m, E.R(o), act=act, cmap=cm, trainable=trainable, name=f"layer.{i}")
+                o = g.buffer(f"layer.{i}", hh, ww, E.rup(conv.out_channels, 8))
+                g.conv(x, conv, E.R(o), act=act, cmap=cm, trainable=trainable, name=f"layer.{i}")
                 x = E.R(o)
                 i += 2 if act == A.ACT_LRELU else 1
                 continue
-            if isinstance(m, ResnetBlock):
-                c0, c2 = m.conv[0], m.conv[2]
+            if isinstance(m, (ResnetBlock, ResnetSNBlock)):
+                c0, c2 = _conv_of(m.conv[0]), _conv_of(m.conv[2])
                 h = g.buffer(f"layer.{i}.h", x.H, x.W, E.rup(c0.out_channels, 8))
                 g.conv(x, c0, E.R(h), act=A.ACT_LRELU, trainable=trainable, name=f"layer.{i}.conv.0")
                 o = g.buffer(f"layer.{i}.out", x.H, x.W, E.rup(c2.out_channels, 8))
@@ -122,6 +189,52 @@ class _PlanDiscriminator(FlatParams, nn.Module):
     def _on_moved(self):
         self._pool.clear()
 
+    # ---- SpectralNorm (nets/SpectralNorm.py:23-35 and its autograd) ----
+    def _sn_state(self, plan, dev):
+        sizes = [1 + s.h + s.width for s in self._sn]
+        st = plan.__dict__.get("sn_state")
+        if st is None:
+            st = torch.zeros(sum(sizes), dtype=torch.float32, device=dev)
+            plan.sn_state = st
+        return st, sizes
+
+    def _sn_forward(self, plan, dev):
+        """power iteration of every SN layer (u, v updated in place; the values used saved in
+        the plan's state for its backward) and W_bar / sigma into module.weight"""
+        st, sizes = self._sn_state(plan, dev)
+        arr = (L.SnLayer * len(self._sn))()
+        off = 0
+        for d, s, n in zip(arr, self._sn, sizes):
+            m = s.module
+            d.w_bar, d.u, d.v = m.weight_bar.data_ptr(), m.weight_u.data_ptr(), m.weight_v.data_ptr()
+            d.w_eff = m.weight.data_ptr()
+            d.state_off, d.h, d.width, d.power_iterations = off, s.h, s.width, s.power_iterations
+            off += n
+        L.check(L.load().dvie_sn_fwd(ctypes.addressof(arr), len(self._sn), st.data_ptr(), L.stream_ptr(dev)),
+                "spectral norm forward")
+
+    def _sn_backward(self, plan, accumulate, dev):
+        """d(W_bar / sigma) (the plan's weight gradient of module.weight) -> weight_bar.grad,
+        and u / v gradients once they are trainable (InterGANNet's set_net_grad(True))"""
+        st, sizes = self._sn_state(plan, dev)
+        todo, off = [], 0
+        for s, n in zip(self._sn, sizes):
+            m = s.module
+            if m.weight_bar.grad is not None and m.weight.grad is not None:
+                todo.append((s, off))
+            off += n
+        if not todo:
+            return
+        arr = (L.SnLayer * len(todo))()
+        for d, (s, o) in zip(arr, todo):
+            m = s.module
+            d.w_bar, d.g_eff, d.g_bar = m.weight_bar.data_ptr(), m.weight.grad.data_ptr(), m.weight_bar.grad.data_ptr()
+            d.g_u = m.weight_u.grad.data_ptr() if m.weight_u.grad is not None else None
+            d.g_v = m.weight_v.grad.data_ptr() if m.weight_v.grad is not None else None
+            d.state_off, d.h, d.width, d.beta = o, s.h, s.width, int(accumulate)
+        L.check(L.load().dvie_sn_bwd(ctypes.addressof(arr), len(todo), st.data_ptr(), L.stream_ptr(dev)),
+                "spectral norm backward")
+
     def run_forward(self, inputs, train):
         x = inputs[0]
         L.require_gpu(x)
@@ -132,12 +245,20 @@ class _PlanDiscriminator(FlatParams, nn.Module):
         backward = trainable or any(in_grads)
         key = (n, H, W, self.dtype, self.training, trainable, in_grads, backward, x.device)
         plan = self._pool.acquire(key)
+        if self._sn:  # the reference updates u, v on every call, train or eval
+            self._sn_forward(plan, x.device)
         for k, t in enumerate(inputs):
             plan.set_input(f"in{k}", t)
-        hb = plan.g.heads["score"]
-        rows = n * (hb.H // self.pool) * (hb.W // self.pool)
-        out = torch.empty(rows, dtype=torch.float32, device=x.device)
-        plan.set_head_output("score", out)
+        if self.local:
+            region, c = plan.g.outputs["score"]
+            buf = torch.empty((n, region.H, region.W, region.buf.C), dtype=torch.float32, device=x.device)
+            plan.set_output("score", buf)
+            out = buf.permute(0, 3, 1, 2)[:, :c]
+        else:
+            hb = plan.g.heads["score"]
+            rows = n * (hb.H // self.pool) * (hb.W // self.pool)
+            out = torch.empty(rows, dtype=torch.float32, device=x.device)
+            plan.set_head_output("score", out)
         plan.run_forward()
         self.last_plan = plan
         if self.training:  # one increment per BatchNorm call, as nn.BatchNorm2d.train()
@@ -148,9 +269,17 @@ class _PlanDiscriminator(FlatParams, nn.Module):
 
     def run_backward(self, plan, inputs, grads, needs):
         (go,) = grads
-        if any(p.requires_grad for p in self.parameters()):
-            plan.set_param_grads(self.grad_views())
-        plan.set_head_grad("score", go.float())
+        dev = inputs[0].device
+        trainable = any(p.requires_grad for p in self.parameters())
+        accumulate = False
+        if trainable:
+            accumulate = self.grad_views()
+            # SN convs: this call's d(W_bar / sigma) overwrites module.weight.grad (scratch)
+            plan.set_param_grads(accumulate, fresh={id(s.module) for s in self._sn})
+        if self.local:
+            plan.set_output_grad("score", go.float())
+        else:
+            plan.set_head_grad("score", go.float())
         outs = []
         for k, t in enumerate(inputs):
             if f"in{k}" in plan.ext_grad:
@@ -160,6 +289,8 @@ class _PlanDiscriminator(FlatParams, nn.Module):
             else:
                 outs.append(None)
         plan.run_backward()
+        if trainable and self._sn:
+            self._sn_backward(plan, accumulate, dev)
         return outs
 
     def activation_signs(self):
@@ -172,24 +303,11 @@ class _PlanDiscriminator(FlatParams, nn.Module):
         return PlanFunction.apply(self, len(ins), *ins, *params)
 
 
-class FrameDiscriminator(_PlanDiscriminator):
-    """Reference nets/FrameDisc.py:35-75."""
-
-    def __init__(self, args):
-        super().__init__()
+class _FrameBase(_PlanDiscriminator):
+    def _setup(self, args):
         self.args = args
         self.seg_disc = bool(getattr(args, "seg_disc", False))
         self.input_dim = 23 if self.seg_disc else 3
-        self.layer = nn.Sequential(
-            Conv2d(self.input_dim, 16, 3, 1, 1), nn.LeakyReLU(0.2, inplace=False),
-            Conv2d(16, 32, 5, 1, 2), nn.BatchNorm2d(32), nn.LeakyReLU(0.2, inplace=False),
-            Conv2d(32, 64, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(64, 64, 3),
-            Conv2d(64, 96, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(96, 96, 3),
-            Conv2d(96, 128, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(128, 128, 3),
-            Conv2d(128, 192, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(192, 192, 3),
-            Conv2d(192, 192, 3, 1, 1), nn.AvgPool2d(8))
-        self.out_c, self.pool = 192, 8
-        self._finish_init()
 
     def _in_widths(self):
         return [3, 20] if self.seg_disc else [3]
@@ -198,25 +316,11 @@ class FrameDiscriminator(_PlanDiscriminator):
         return self._run(x, seg) if self.seg_disc else self._run(x)
 
 
-class VideoDiscriminator(_PlanDiscriminator):
-    """Reference nets/VidDisc.py:34-84."""
-
-    def __init__(self, args):
-        super().__init__()
+class _VideoBase(_PlanDiscriminator):
+    def _setup(self, args):
         self.args = args
         self.seg_disc = bool(getattr(args, "seg_disc", False))
         self.input_dim = 23 if self.seg_disc else 3
-        self.layer = nn.Sequential(
-            Conv2d(3 * self.input_dim, 32, 3, 1, 1), nn.LeakyReLU(0.2, inplace=False),
-            Conv2d(32, 64, 5, 1, 2), nn.BatchNorm2d(64), nn.LeakyReLU(0.2, inplace=False),
-            Conv2d(64, 32, 3, 1, 1), nn.BatchNorm2d(32), nn.LeakyReLU(0.2, inplace=False),
-            Conv2d(32, 32, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(32, 32, 3),
-            Conv2d(32, 64, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(64, 64, 3),
-            Conv2d(64, 128, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(128, 128, 3),
-            Conv2d(128, 256, 3, 2, 1), nn.LeakyReLU(0.2, inplace=True), ResnetBlock(256, 256, 3),
-            Conv2d(256, 256, 3, 1, 1), nn.AvgPool2d(8))
-        self.out_c, self.pool = 256, 8
-        self._finish_init()
 
     def _in_widths(self):
         return [3, 20, 6, 40] if self.seg_disc else [3, 6]
@@ -225,3 +329,169 @@ class VideoDiscriminator(_PlanDiscriminator):
         if self.seg_disc:
             return self._run(x, seg, input_x, input_seg)
         return self._run(x, input_x)
+
+
+def _lr(inplace=True):
+    return nn.LeakyReLU(0.2, inplace=inplace)
+
+
+def _sn(*a):
+    return SpectralNorm(Conv2d(*a))
+
+
+class FrameDiscriminator(_FrameBase):
+    """Reference nets/FrameDisc.py:35-75."""
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            Conv2d(self.input_dim, 16, 3, 1, 1), _lr(False),
+            Conv2d(16, 32, 5, 1, 2), nn.BatchNorm2d(32), _lr(False),
+            Conv2d(32, 64, 3, 2, 1), _lr(), ResnetBlock(64, 64, 3),
+            Conv2d(64, 96, 3, 2, 1), _lr(), ResnetBlock(96, 96, 3),
+            Conv2d(96, 128, 3, 2, 1), _lr(), ResnetBlock(128, 128, 3),
+            Conv2d(128, 192, 3, 2, 1), _lr(), ResnetBlock(192, 192, 3),
+            Conv2d(192, 192, 3, 1, 1), nn.AvgPool2d(8))
+        self.out_c, self.pool = 192, 8
+        self._finish_init()
+
+
+class FrameLocalDiscriminator(_FrameBase):
+    """Reference nets/FrameDisc.py:77-114 (output: the (B, 1, H/4, W/4) map)."""
+    local = True
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            Conv2d(self.input_dim, 16, 3, 1, 1), _lr(False),
+            Conv2d(16, 32, 5, 1, 2), nn.BatchNorm2d(32), _lr(False),
+            Conv2d(32, 64, 3, 2, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 64, 3, 1, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 128, 3, 2, 1), nn.BatchNorm2d(128), _lr(),
+            Conv2d(128, 128, 3, 1, 1), nn.BatchNorm2d(128), _lr(),
+            Conv2d(128, 64, 3, 1, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 1, 1, 1, 0))
+        self._finish_init()
+
+
+class FrameSNDiscriminator(_FrameBase):
+    """Reference nets/FrameDisc.py:116-156."""
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            _sn(self.input_dim, 16, 3, 1, 1), _lr(False),
+            _sn(16, 32, 5, 1, 2), _lr(False),
+            _sn(32, 64, 3, 2, 1), _lr(), ResnetSNBlock(64, 64, 3),
+            _sn(64, 96, 3, 2, 1), _lr(), ResnetSNBlock(96, 96, 3),
+            _sn(96, 128, 3, 2, 1), _lr(), ResnetSNBlock(128, 128, 3),
+            _sn(128, 128, 3, 1, 1), nn.AvgPool2d(16))
+        self.out_c, self.pool = 128, 16
+        self._finish_init()
+
+
+class FrameSNLocalDiscriminator(_FrameBase):
+    """Reference nets/FrameDisc.py:158-189 (output: the (B, 1, H/4, W/4) map)."""
+    local = True
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            _sn(self.input_dim, 16, 3, 1, 1), _lr(False),
+            _sn(16, 32, 5, 1, 2), _lr(False),
+            _sn(32, 64, 3, 2, 1), _lr(),
+            _sn(64, 64, 3, 1, 1), _lr(),
+            _sn(64, 128, 3, 2, 1), _lr(),
+            _sn(128, 128, 3, 1, 1), _lr(),
+            _sn(128, 64, 3, 1, 1), _lr(),
+            _sn(64, 1, 1, 1, 0))
+        self._finish_init()
+
+
+class VideoDiscriminator(_VideoBase):
+    """Reference nets/VidDisc.py:34-84."""
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            Conv2d(3 * self.input_dim, 32, 3, 1, 1), _lr(False),
+            Conv2d(32, 64, 5, 1, 2), nn.BatchNorm2d(64), _lr(False),
+            Conv2d(64, 32, 3, 1, 1), nn.BatchNorm2d(32), _lr(False),
+            Conv2d(32, 32, 3, 2, 1), _lr(), ResnetBlock(32, 32, 3),
+            Conv2d(32, 64, 3, 2, 1), _lr(), ResnetBlock(64, 64, 3),
+            Conv2d(64, 128, 3, 2, 1), _lr(), ResnetBlock(128, 128, 3),
+            Conv2d(128, 256, 3, 2, 1), _lr(), ResnetBlock(256, 256, 3),
+            Conv2d(256, 256, 3, 1, 1), nn.AvgPool2d(8))
+        self.out_c, self.pool = 256, 8
+        self._finish_init()
+
+
+class VideoLocalDiscriminator(_VideoBase):
+    """Reference nets/VidDisc.py:86-138 (output: the (B, 1, H/16, W/16) map)."""
+    local = True
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            Conv2d(3 * self.input_dim, 64, 1, 1, 0), _lr(False),
+            Conv2d(64, 64, 3, 1, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 64, 3, 2, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 64, 3, 1, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 64, 3, 1, 1), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 128, 3, 2, 1), nn.BatchNorm2d(128), _lr(),
+            Conv2d(128, 128, 3, 1, 1), nn.BatchNorm2d(128), _lr(),
+            Conv2d(128, 128, 3, 2, 1), nn.BatchNorm2d(128), _lr(),
+            Conv2d(128, 128, 3, 1, 1), nn.BatchNorm2d(128), _lr(),
+            Conv2d(128, 256, 3, 2, 1), nn.BatchNorm2d(256), _lr(),
+            Conv2d(256, 256, 3, 1, 1), nn.BatchNorm2d(256), _lr(),
+            Conv2d(256, 64, 1, 1, 0), nn.BatchNorm2d(64), _lr(),
+            Conv2d(64, 1, 1, 1, 0))
+        self._finish_init()
+
+
+class VideoSNDiscriminator(_VideoBase):
+    """Reference nets/VidDisc.py:140-183."""
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            _sn(3 * self.input_dim, 32, 3, 1, 1), _lr(False),
+            _sn(32, 64, 5, 1, 2), _lr(False),
+            _sn(64, 32, 3, 1, 1), _lr(False),
+            _sn(32, 32, 3, 2, 1), _lr(), ResnetSNBlock(32, 32, 3),
+            _sn(32, 64, 3, 2, 1), _lr(), ResnetSNBlock(64, 64, 3),
+            _sn(64, 128, 3, 2, 1), _lr(), ResnetSNBlock(128, 128, 3),
+            _sn(128, 128, 3, 1, 1), nn.AvgPool2d(16))
+        self.out_c, self.pool = 128, 16
+        self._finish_init()
+
+
+class VideoSNLocalDiscriminator(_VideoBase):
+    """Reference nets/VidDisc.py:185-226 (output: the (B, 1, H/16, W/16) map)."""
+    local = True
+
+    def __init__(self, args):
+        super().__init__()
+        self._setup(args)
+        self.layer = nn.Sequential(
+            _sn(3 * self.input_dim, 64, 1, 1, 0), _lr(False),
+            _sn(64, 64, 3, 1, 1), _lr(),
+            _sn(64, 64, 3, 2, 1), _lr(),
+            _sn(64, 64, 3, 1, 1), _lr(),
+            _sn(64, 64, 3, 1, 1), _lr(),
+            _sn(64, 128, 3, 2, 1), _lr(),
+            _sn(128, 128, 3, 1, 1), _lr(),
+            _sn(128, 128, 3, 2, 1), _lr(),
+            _sn(128, 128, 3, 1, 1), _lr(),
+            _sn(128, 256, 3, 2, 1), _lr(),
+            _sn(256, 256, 3, 1, 1), _lr(),
+            _sn(256, 64, 1, 1, 0), _lr(),
+            _sn(64, 1, 1, 1, 0))
+        self._finish_init()

@@ -47,6 +47,8 @@ class _FusedOptimizer(torch.optim.Optimizer):
             g = p.grad
             if g is None or g.data_ptr() != fg.data_ptr() + (p.data_ptr() - flat.data_ptr()):
                 return None
+        if len({float(self.state[p]["step"]) if "step" in self.state[p] else 0.0 for p in ps}) > 1:
+            return None  # per-parameter step counts differ (SN u, v become trainable after step 1)
         k0, k1 = self.STATE
         ent = self._flat.get(gi)
         if ent is None or ent[1].device != flat.device or ent[1].numel() != flat.numel():

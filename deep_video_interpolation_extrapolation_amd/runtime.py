@@ -73,6 +73,8 @@ class FlatParams:
         fg = self.flat_grad()
         accumulate = False
         for p, (off, n, shape) in zip(self._flat_params, self._flat_specs):
+            if not p.requires_grad:  # frozen (e.g. SpectralNorm u, v): .grad stays None
+                continue
             if p.grad is None:
                 p.grad = fg[off:off + n].view(shape)
             else:

@@ -381,6 +381,38 @@ int dvie_adam(float* p, const float* g, float* m, float* v, long long n, float s
               float eps, float wd, void* stream);
 
 /*
+ * SpectralNorm (reference nets/SpectralNorm.py:10-68), fp32, one workgroup per layer.
+ * W_bar is the (h, width) row-major view of the OIHW weight (width = cin*kh*kw).
+ * Forward (SpectralNorm._update_u_v, l.23-35), `power_iterations` times:
+ *   v = l2normalize(W_bar^T u); u = l2normalize(W_bar v)      (l2normalize: x / (|x| + 1e-12))
+ * then sigma = u . (W_bar v) and w_eff = W_bar / sigma.  u and v are updated in place; the
+ * values used ([sigma, u(h), v(width)]) are saved at state + state_off for the backward.
+ * Backward (autograd of `w / sigma` with sigma = u.dot(W_bar.mv(v))),
+ * g_sigma = -sum(g_eff * W_bar) / sigma^2:
+ *   g_bar (+)= g_eff / sigma + g_sigma * u v^T
+ *   g_u   (+)= g_sigma * (W_bar v),  g_v (+)= g_sigma * (W_bar^T u)   (only if non-null: u and v
+ *   become trainable in the reference once set_net_grad(True) ran, nets/InterGANNet.py:81)
+ * beta = 1 accumulates into g_bar / g_u / g_v.  u, v here are the values the forward saved.
+ * Replaces: SpectralNorm.forward's _update_u_v (l.66-68) and its autograd backward.
+ * `n` layers (host array, any count), one workgroup each.
+ */
+typedef struct dvie_sn_layer {
+  const float* w_bar;
+  float* u;
+  float* v;
+  float* w_eff;
+  const float* g_eff;
+  float* g_bar;
+  float* g_u;
+  float* g_v;
+  long long state_off;
+  int h, width, power_iterations, beta;
+} dvie_sn_layer;
+
+int dvie_sn_fwd(const dvie_sn_layer* layers, int n, float* state, void* stream);
+int dvie_sn_bwd(const dvie_sn_layer* layers, int n, const float* state, void* stream);
+
+/*
  * Op-list executor: runs n descriptors in order on one stream with a single host call
  * (the per-step forward and backward plans of the HRNet / VGG executors).
  */

@@ -81,6 +81,11 @@ def disc_inputs(n=2, H=128, W=256, seed=21):
     return x, seg, ix, iseg, gout
 
 
+def disc_map_grad(shape, seed=27):
+    """upstream gradient of a local (map-output) discriminator"""
+    return torch.randn(shape, generator=_gen(seed))
+
+
 def sample_idx(numel, k=256, seed=99):
     """fixed sample positions for large-tensor fixtures"""
     return torch.randint(0, numel, (k,), generator=_gen(seed))

@@ -203,9 +203,56 @@ def g7():
                         bufs=np.concatenate([bufs[k].numpy().reshape(-1) for k in sorted(bufs)]))
 
 
+G8_CASES = (("FrameLocalDiscriminator", 51), ("FrameSNDiscriminator", 52), ("FrameSNLocalDiscriminator", 53),
+            ("VideoLocalDiscriminator", 54), ("VideoSNDiscriminator", 55), ("VideoSNLocalDiscriminator", 56))
+
+
+def g8():
+    """the remaining discriminator variants (local map outputs, SpectralNorm) at 128x128,
+    seg_disc, train mode: one forward + backward each; `uvgrad` repeats the SN ones with every
+    parameter requiring grad (the state after InterGANNet's set_net_grad(True))."""
+    out = {}
+    for cls, seed in G8_CASES:
+        for uvgrad in ((False, True) if "SN" in cls else (False,)):
+            t = cls + ("_uvgrad" if uvgrad else "")
+            torch.manual_seed(seed)
+            d = ref_nets.__dict__[cls](args_ns(seg_disc=True))
+            d.train()
+            if uvgrad:
+                for p in d.parameters():
+                    p.requires_grad = True
+            x, seg, ix, iseg, gout = inputs.disc_inputs(2, 128, 128)
+            ins = [x, seg] + ([ix, iseg] if cls.startswith("Video") else [])
+            ins = [v.clone().requires_grad_(True) for v in ins]
+            score = d(*ins)
+            if score.dim() > 1:
+                gout = inputs.disc_map_grad(tuple(score.shape))
+            score.backward(gout)
+            out[t + "_score"] = score.detach().numpy()
+            for k, v in enumerate(ins):
+                gv = v.grad.double().reshape(-1)
+                out[t + f"_gin{k}"] = np.concatenate([[float(gv.sum()), float(gv.abs().sum()), float(gv.norm())],
+                                                      gv[inputs.sample_idx(gv.numel())].numpy()])
+            named = dict(d.named_parameters())
+            names = sorted(n for n in named if named[n].grad is not None)
+            out[t + "_param_names"] = np.array(names)
+            out[t + "_grad_stats"] = np.array([[float(named[n].grad.double().sum()),
+                                                float((named[n].grad.double() ** 2).sum())] for n in names])
+            sd = d.state_dict()
+            uv = sorted(k for k in sd if k.endswith("weight_u") or k.endswith("weight_v"))
+            if uv:  # u, v after the forward's power iteration
+                out[t + "_uv_names"] = np.array(uv)
+                out[t + "_uv"] = np.concatenate([sd[k].numpy().reshape(-1) for k in uv])
+            bufs = {k: v for k, v in sd.items() if "running" in k}
+            if bufs:
+                out[t + "_buf_names"] = np.array(sorted(bufs))
+                out[t + "_bufs"] = np.concatenate([bufs[k].numpy() for k in sorted(bufs)])
+    np.savez_compressed(os.path.join(HERE, "disc_sn.npz"), **out)
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()

@@ -86,6 +86,62 @@ def test_disc_fp32_matches_oracle(dev, kind, seed, hw):
     assert int(sd[list(stats)[0] + ".num_batches_tracked"]) == 1
 
 
+VARIANTS = [("FrameLocalDiscriminator", 51), ("FrameSNDiscriminator", 52), ("FrameSNLocalDiscriminator", 53),
+            ("VideoLocalDiscriminator", 54), ("VideoSNDiscriminator", 55), ("VideoSNLocalDiscriminator", 56)]
+
+
+@pytest.mark.parametrize("cls,seed", VARIANTS)
+@pytest.mark.parametrize("uvgrad", [False, True])
+def test_disc_variant_fp32_matches_oracle(dev, cls, seed, uvgrad):
+    """Local (map output) and SpectralNorm discriminators (HIP power iteration + sigma
+    adjoint, dvie_sn_fwd / dvie_sn_bwd) vs the fp64 oracle (itself pinned to G8) on the HIP
+    run's LeakyReLU branches: output 1e-5, input / parameter gradients 2e-4 relative L2,
+    u / v after the power iteration 1e-5.  uvgrad: u / v trainable (after set_net_grad(True))."""
+    if uvgrad and "SN" not in cls:
+        pytest.skip("no SpectralNorm")
+    os.environ["DVIE_PRECISION"] = "fp32"
+    from deep_video_interpolation_extrapolation_amd import nets
+    from test_oracle_disc import run_variant
+    torch.manual_seed(seed)
+    d = nets.__dict__[cls](types.SimpleNamespace(seg_disc=True, precision="fp32")).to(dev)
+    P = OD.init_params(OD.SPECS[cls](23), seed)
+    sd = d.state_dict()
+    assert set(P) <= set(sd)
+    for k, v in P.items():
+        assert torch.equal(sd[k].cpu(), v), k
+    if uvgrad:
+        for p in d.parameters():
+            p.requires_grad = True
+    x, seg, ix, iseg, gout = inputs.disc_inputs(2, 128, 128)
+    ins = [x, seg] + ([ix, iseg] if cls.startswith("Video") else [])
+    gins = [v.to(dev).requires_grad_(True) for v in ins]
+    got = d(*gins)
+    if got.dim() > 1:
+        gout = inputs.disc_map_grad(tuple(got.shape))
+    got.backward(gout.to(dev))
+    torch.cuda.synchronize()
+    ref, oins, params, _, _, _ = run_variant(cls, seed, uvgrad, torch.float64, masks=d.activation_signs())
+    assert tuple(got.shape) == tuple(ref.shape)
+    e = rel_l2(got.detach(), ref.detach())
+    assert e < 1e-5, e
+    for a, b in zip(gins, oins):
+        e = rel_l2(a.grad, b.grad)
+        assert e < 2e-4, e
+    named = dict(d.named_parameters())
+    sd = d.state_dict()
+    for k, v in params.items():
+        if k.endswith(("weight_u", "weight_v")):
+            assert rel_l2(sd[k], v.detach()) < 1e-5, k
+        if v.grad is None:
+            assert named[k].grad is None, k
+            continue
+        if k.endswith(".bias") and f"layer.{int(k.split('.')[1]) + 1}.running_mean" in P:
+            assert float(named[k].grad.abs().max()) < 1e-4, k  # conv bias before BatchNorm: zero gradient
+            continue
+        e = rel_l2(named[k].grad, v.grad)
+        assert e < 2e-4, (k, e)
+
+
 @pytest.mark.parametrize("kind,seed", [("frame", 31), ("video", 32)])
 def test_disc_bf16_close_to_fp32(dev, kind, seed):
     x, seg, ix, iseg, gout = inputs.disc_inputs(2, 128, 256)

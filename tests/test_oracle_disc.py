@@ -62,6 +62,63 @@ def test_disc_oracle_matches_reference(tag, spec_fn, seed, hw):
     np.testing.assert_allclose(ev.numpy(), f[t + "_score_eval"], rtol=1e-4, atol=1e-5)
 
 
+G8 = [("FrameLocalDiscriminator", 51), ("FrameSNDiscriminator", 52), ("FrameSNLocalDiscriminator", 53),
+      ("VideoLocalDiscriminator", 54), ("VideoSNDiscriminator", 55), ("VideoSNLocalDiscriminator", 56)]
+
+
+def run_variant(cls, seed, uvgrad, dtype=torch.float32, masks=None):
+    """oracle forward + backward of a G8 variant at 128x128 (seg_disc); `uvgrad`: SpectralNorm
+    u / v require grad (the state after InterGANNet's set_net_grad(True))"""
+    spec = OD.SPECS[cls](23)
+    P = OD.init_params(spec, seed)
+    stats = {k[:-len(".running_mean")]: (P[k].clone().to(dtype), P[k[:-4] + "var"].clone().to(dtype))
+             for k in P if k.endswith("running_mean")}
+    x, seg, ix, iseg, gout = inputs.disc_inputs(2, 128, 128)
+    ins = [x, seg] + ([ix, iseg] if cls.startswith("Video") else [])
+    ins = [v.clone().to(dtype).requires_grad_(True) for v in ins]
+    params = {k: v.clone().to(dtype).requires_grad_(uvgrad or not k.endswith(("weight_u", "weight_v")))
+              for k, v in P.items() if "running" not in k}
+    out = OD.forward(params, spec, torch.cat(ins, 1), training=True, stats=stats, masks=masks)
+    if out.dim() > 1:
+        gout = inputs.disc_map_grad(tuple(out.shape))
+    out.backward(gout.to(dtype))
+    return out, ins, params, stats, P, gout
+
+
+@pytest.mark.parametrize("cls,seed", G8)
+@pytest.mark.parametrize("uvgrad", [False, True])
+def test_disc_variant_oracle_matches_reference(cls, seed, uvgrad):
+    """local (map output) and SpectralNorm discriminators vs tests/golden/disc_sn.npz (G8):
+    output, input gradients, parameter gradients (u / v ones too once trainable), u / v after
+    the forward's power iteration, BatchNorm running statistics."""
+    if uvgrad and "SN" not in cls:
+        pytest.skip("no SpectralNorm")
+    f = np.load(os.path.join(G, "disc_sn.npz"))
+    t = cls + ("_uvgrad" if uvgrad else "")
+    out, ins, params, stats, _, _ = run_variant(cls, seed, uvgrad)
+    np.testing.assert_allclose(out.detach().numpy(), f[t + "_score"], rtol=1e-4, atol=1e-5)
+    for k, v in enumerate(ins):
+        gv = v.grad.double().reshape(-1)
+        got = gv[inputs.sample_idx(gv.numel())].numpy()
+        ref = f[t + f"_gin{k}"]
+        assert np.abs(got - ref[3:]).max() / (np.abs(ref[3:]).max() + 1e-30) < 1e-3, k
+        np.testing.assert_allclose([float(gv.abs().sum()), float(gv.norm())], ref[1:3], rtol=1e-3)
+    names = [str(n) for n in f[t + "_param_names"]]
+    assert sorted(n for n, p in params.items() if p.grad is not None) == names
+    g2 = np.array([float((params[n].grad.double() ** 2).sum()) for n in names])
+    ref2 = f[t + "_grad_stats"][:, 1]
+    ok = np.abs(g2 - ref2) <= 1e-3 * ref2 + 1e-12  # BatchNorm-preceding conv biases: ~0
+    assert ok.all(), [n for n, o in zip(names, ok) if not o]
+    if t + "_uv_names" in f.files:
+        uv = np.concatenate([params[str(k)].detach().numpy().reshape(-1) for k in f[t + "_uv_names"]])
+        np.testing.assert_allclose(uv, f[t + "_uv"], rtol=1e-4, atol=1e-6)
+    if t + "_buf_names" in f.files:
+        bufs = np.concatenate([stats[k[:-len(".running_mean")]][0].numpy() if k.endswith("running_mean")
+                               else stats[k[:-len(".running_var")]][1].numpy()
+                               for k in [str(b) for b in f[t + "_buf_names"]]])
+        np.testing.assert_allclose(bufs, f[t + "_bufs"], rtol=1e-4, atol=1e-6)
+
+
 def test_adam_101_matches_torch_adam_at_zero_eps():
     """The 1.0.1 Adam form and torch 2.x Adam differ only in where eps enters
     (sqrt(v) + eps vs sqrt(v)/sqrt(bc2) + eps): with eps = 0 they must agree."""
