@@ -239,11 +239,13 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const dvie_wgrad_desc p, lon
     }
 }
 
-// 32 float4 columns x 8 split-lanes per block: every thread streams every 8th slab of its
-// 16-byte column (coalesced 512-byte rows per slab), fp64 accumulation, LDS fold, scatter
-// into the OIHW gradient.
+// QB float4 columns x SL split-lanes per block (QB * SL = 256): every thread streams every
+// SL-th slab of its 16-byte column (coalesced rows per slab), fp64 accumulation, LDS fold,
+// scatter into the OIHW gradient.  Wide reductions (weights) use 32 x 8; narrow ones with
+// many slabs (bias column sums: cout/4 columns, thousands of partials) 4 x 64.
+template <int QB, int SL>
 __global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p) {
-  constexpr int QB = 32, SL = 8;
+  static_assert(QB * SL == 256, "block shape");
   __shared__ double red[SL][QB][4];
   const int tid = threadIdx.x;
   const int ql = tid % QB, sl = tid / QB;
@@ -300,7 +302,20 @@ __global__ __launch_bounds__(256) void colsum_kernel(const dvie_colsum_desc p, l
     const int rl = tid / (256 / nrl);
     f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
     if (q < cq && rl < nrl) {
-      for (long long r = rbeg + rl; r < rend; r += nrl) s += V4<T>::load((const T*)p.g + r * p.g_ld + 4 * q);
+      // four independent row streams per thread: four loads in flight per iteration
+      const T* g = (const T*)p.g + 4 * q;
+      f32x4 s1 = s, s2 = s, s3 = s;
+      long long r = rbeg + rl;
+      for (; r + 3 * nrl < rend; r += 4 * nrl) {
+        const f32x4 a = V4<T>::load(g + r * p.g_ld), b = V4<T>::load(g + (r + nrl) * p.g_ld);
+        const f32x4 c = V4<T>::load(g + (r + 2 * nrl) * p.g_ld), d = V4<T>::load(g + (r + 3 * nrl) * p.g_ld);
+        s += a;
+        s1 += b;
+        s2 += c;
+        s3 += d;
+      }
+      for (; r < rend; r += nrl) s += V4<T>::load(g + r * p.g_ld);
+      s += (s1 + s2) + s3;
     }
     for (int e = 0; e < 4; ++e) red[tid * 4 + e] = s[e];
     __syncthreads();
@@ -389,9 +404,13 @@ int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream) {
                  "wreduce: slab alignment (ws_rows*ws_k and co_off*ws_k multiples of 4)");
   DVIE_CHECK_ARG(d->co_off + d->cout_p <= d->ws_rows, "wreduce: rows");
   const long long total4 = (long long)(d->ws_rows - d->co_off) * d->ws_k / 4;
-  const int blocks = (int)((total4 + 31) / 32);
-  if (blocks < 1) return DVIE_OK;
-  hipLaunchKernelGGL(wreduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *d);
+  if (total4 < 1) return DVIE_OK;
+  if (total4 < 2048 && d->splits >= 256)
+    hipLaunchKernelGGL((wreduce_kernel<4, 64>), dim3((unsigned)((total4 + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       *d);
+  else
+    hipLaunchKernelGGL((wreduce_kernel<32, 8>), dim3((unsigned)((total4 + 31) / 32)), dim3(256), 0,
+                       (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
 

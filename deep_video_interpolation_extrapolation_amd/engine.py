@@ -874,7 +874,7 @@ class Plan:
             self.bwd.append(o)
             self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
             if lay.has_bias:
-                csplits = max(1, min(512, npix // 2048))
+                csplits = max(1, min(2048, npix // 512))  # >= 8 blocks per CU at full resolution
                 o = self._op(L.OP_COLSUM)
                 cd = o.u.colsum
                 cd.g, cd.ws, cd.g_ld, cd.rows, cd.c, cd.splits, cd.dtype = gout, 0, gld, npix, lay.cout_p, csplits, self.dt
