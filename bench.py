@@ -75,6 +75,40 @@ def cpu_baseline(H, W):
                       f"{dt:.1f}s"}
 
 
+def warp_roofline(dev, n, H, W, reps=20):
+    """The optical-flow warp (FlowWrapper, utils/net_utils.py:89-114; dormant in the
+    InterNet step) on (n, 3, H, W) frames: forward and backward timed with HIP events on the
+    launch stream, against the HBM roofline.  Algorithmic bytes per pixel (fp32): forward
+    img 12 + flow 8 + out 12 = 32; backward img 12 + flow 8 + dout 12 + dimg 12 + dflow 8 = 52."""
+    from deep_video_interpolation_extrapolation_amd.utils.net_utils import flow_warp
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.rand((n, 3, H, W), generator=g, device=dev).requires_grad_(True)
+    flow = ((torch.rand((n, 2, H, W), generator=g, device=dev) * 2 - 1) * 0.05).requires_grad_(True)
+    go = torch.randn((n, 3, H, W), generator=g, device=dev)
+    for _ in range(3):
+        flow_warp(x, flow).backward(go)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    tf = tb = 0.0
+    for _ in range(reps):
+        x.grad = flow.grad = None
+        ev[0].record()
+        y = flow_warp(x, flow)
+        ev[1].record()
+        y.backward(go)
+        ev[2].record()
+        torch.cuda.synchronize()
+        tf += ev[0].elapsed_time(ev[1])
+        tb += ev[1].elapsed_time(ev[2])
+    px = n * H * W
+    fwd = 32.0 * px / (tf / reps * 1e-3) / 1e9
+    bwd = 52.0 * px / (tb / reps * 1e-3) / 1e9
+    return {"shape": [n, 3, H, W], "fwd_ms": round(tf / reps, 4), "bwd_ms": round(tb / reps, 4),
+            "fwd_GBps": round(fwd, 1), "bwd_GBps": round(bwd, 1), "fwd_frac": round(fwd / PEAK_HBM_GBS, 4),
+            "bwd_frac": round(bwd / PEAK_HBM_GBS, 4), "bytes_per_px": {"fwd": 32, "bwd": 52},
+            "note": "bwd includes the zero-fill of dimg (torch.zeros) that its atomics accumulate into"}
+
+
 def main():
     a = parse()
     os.environ["DVIE_PRECISION"] = a.precision
@@ -198,6 +232,7 @@ def main():
             "loss_all": loss_all,
             "step_breakdown_ms": {k: round(v["ms"] / max(1, a.profile_steps), 3) for k, v in sorted(agg.items())},
         }
+        out["warp"] = warp_roofline(dev, a.batch, a.height, a.width)
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.height, a.width)
         else:
