@@ -175,7 +175,8 @@ EXPORTS = [
     "dvie_ew", "dvie_loss", "dvie_loss_partial_count", "dvie_loss_ws_floats", "dvie_warp_fwd",
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
-    "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd",
+    "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
+    "dvie_reparam_bwd",
 ]
 
 _lib = None
@@ -227,6 +228,9 @@ def load():
         for name in ("dvie_sn_fwd", "dvie_sn_bwd"):
             getattr(lib, name).argtypes = [vp, i32, vp, vp]
             getattr(lib, name).restype = i32
+        lib.dvie_reparam_fwd.argtypes = [vp, vp, vp, vp, i64, vp]
+        lib.dvie_reparam_bwd.argtypes = [vp, vp, vp, vp, vp, i64, i32, vp]
+        lib.dvie_reparam_fwd.restype = lib.dvie_reparam_bwd.restype = i32
         _lib = lib
         return lib
 

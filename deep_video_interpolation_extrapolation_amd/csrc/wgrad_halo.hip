@@ -281,6 +281,8 @@ struct WgPlan {
 
 static WgPlan wgrad_plan(const dvie_wgrad_desc& p) {
   if (p.th == 3) return {4, 1, 1};
+  const char* e = getenv("DVIE_WG_TM");  // tuning override for 1x1: "<tmo><tmi>", e.g. "11"
+  if (e && e[0] && e[1]) return {2, e[0] == '2' ? 2 : 1, e[1] == '2' ? 2 : 1};
   return {2, p.cout > 64 ? 2 : 1, p.c > 64 ? 2 : 1};
 }
 
@@ -300,6 +302,8 @@ int wgrad_halo_splits(const dvie_wgrad_desc& p) {
   int tx, ty, nt, nco, nci;
   wgrad_tiles(p, w, tx, ty, nt, nco, nci);
   int s = 256 / (nco * nci);  // one workgroup per CU (LDS-bound): a single wave of workgroups
+  const char* e = getenv("DVIE_WG_SPLITS");  // tuning: multiplier of that split count
+  if (e && *e && atoi(e) > 0) s *= atoi(e);
   if (s > nt) s = nt;
   return s < 1 ? 1 : s;
 }

@@ -94,7 +94,17 @@ class ConvLayer:
         self.m = module
         self.name = name
         w = module.weight
-        self.cout, self.cin, self.kh, self.kw = w.shape
+        # nn.ConvTranspose2d: its (in, out, kh, kw) weight IS the OIHW weight of the conv
+        # out -> in whose data gradient the transposed conv computes ("virtual conv": cout =
+        # the ConvT input channels, cin = its output channels; the bias has cin entries)
+        self.transposed = isinstance(module, torch.nn.ConvTranspose2d)
+        if self.transposed:
+            assert tuple(module.output_padding) == (0, 0), "ConvTranspose2d output_padding"
+        if w.dim() == 2:  # nn.Linear (through LinearAsConv): a 1x1 conv over a (B, 1, 1, in) image
+            self.cout, self.cin = w.shape
+            self.kh = self.kw = 1
+        else:
+            self.cout, self.cin, self.kh, self.kw = w.shape
         self.stride = module.stride[0]
         self.pad = module.padding[0]
         assert module.stride[0] == module.stride[1] and module.padding[0] == module.padding[1]
@@ -156,6 +166,32 @@ class ConvOp(_Op):
 
     def inputs(self):
         return [self.x] + ([self.res] if self.res is not None else [])
+
+
+class ConvTOp(_Op):
+    """nn.ConvTranspose2d (+ activation): x (ConvT input) -> out (ConvT output)."""
+
+    def __init__(self, x, layer, out, act):
+        self.x, self.layer, self.out, self.act, self.res = x, layer, out, act, None
+
+    def inputs(self):
+        return [self.x]
+
+
+class LinearAsConv:
+    """nn.Linear seen by the engine as a 1x1 conv (the same (out, in) weight memory)."""
+    stride, padding, dilation, groups = (1, 1), (0, 0), (1, 1), 1
+
+    def __init__(self, linear):
+        self.lin = linear
+
+    @property
+    def weight(self):
+        return self.lin.weight
+
+    @property
+    def bias(self):
+        return self.lin.bias
 
 
 class FuseOp(_Op):
@@ -284,6 +320,19 @@ class Graph:
         self._add(ConvOp(x, lay, out, act, res))
         return out
 
+    def convT(self, x, module, out, act=L.ACT_NONE, trainable=True, name=""):
+        """nn.ConvTranspose2d: the data gradient of the conv sharing its weight
+        (Conv2d(out_T -> in_T, k, s, p)), run as a forward op; out = (x - 1)*s - 2p + k."""
+        lay = self.layer(module, trainable, name)
+        assert lay.transposed
+        lay.bind_input(out.c, None)
+        assert x.c == lay.cout_p, (name, x.c, lay.cout_p)
+        oh = (out.H + 2 * lay.pad - lay.kh) // lay.stride + 1
+        ow = (out.W + 2 * lay.pad - lay.kw) // lay.stride + 1
+        assert (x.H, x.W) == (oh, ow), (name, x.H, x.W, oh, ow)
+        self._add(ConvTOp(x, lay, out, act))
+        return out
+
     def fuse(self, srcs, out, act=L.ACT_NONE, align=False):
         assert 1 <= len(srcs) <= 3
         for s in srcs:
@@ -387,7 +436,7 @@ class Plan:
                 need = False
                 if isinstance(op, InputOp):
                     need = op.requires_grad
-                elif isinstance(op, ConvOp):
+                elif isinstance(op, (ConvOp, ConvTOp)):
                     need = op.layer.trainable or any(r.buf.needs_grad for r in op.inputs())
                 elif isinstance(op, BNOp):
                     need = op.trainable or op.x.buf.needs_grad
@@ -447,13 +496,15 @@ class Plan:
             ft = lay.fwd_taps()
             descs.append(self._pack_desc(lay, lay.wf, lay.cout_p, kpad, lay.cin_p, 0, ft, cmap_t))
             if lay.has_bias:
-                lay.bias_p = torch.zeros(lay.cout_p, dtype=torch.float32, device=self.device)
+                # (a transposed conv's bias belongs to its output = the virtual conv's input)
+                nbias, rows = (lay.cin, lay.cin_p) if lay.transposed else (lay.cout, lay.cout_p)
+                lay.bias_p = torch.zeros(rows, dtype=torch.float32, device=self.device)
                 self.keep.append(lay.bias_p)
                 d = L.PackDesc()
                 d.src, d.dst, d.cmap = lay.m.bias.data_ptr(), lay.bias_p.data_ptr(), None
-                d.rows, d.kpad, d.c, d.mode = lay.cout_p, 1, 1, 0
+                d.rows, d.kpad, d.c, d.mode = rows, 1, 1, 0
                 d.th, d.tw, d.kh0, d.kw0, d.dkh, d.dkw = 1, 1, 0, 0, 1, 1
-                d.cout_s, d.cin_s, d.kh_s, d.kw_s, d.dtype = lay.cout, 1, 1, 1, L.F32
+                d.cout_s, d.cin_s, d.kh_s, d.kw_s, d.dtype = nbias, 1, 1, 1, L.F32
                 descs.append(d)
             lay.wd = []
         self._pack_descs = descs  # dgrad packs appended during backward build
@@ -560,6 +611,20 @@ class Plan:
                 if ext:
                     self.ext_out.setdefault(out.buf.name, []).append((len(self.fwd), out))
                 self.fwd.append(o)
+            elif isinstance(op, ConvTOp):
+                # the stride phases of the virtual conv's data gradient, over the ConvT input
+                lay, x, out = op.layer, op.x, op.out
+                assert not out.buf.external
+                for ph, wt, kpad in self._dgrad_weights(lay, out.H, out.W):
+                    o = self.conv_desc(
+                        self.ptr(x), x.buf.C, nf, x.H, x.W, lay.cout_p, wt.data_ptr(), kpad, out.c, ph["oh"], ph["ow"],
+                        1, 1, ph, self.ptr(out), out.buf.C, out.H, out.W, osy=lay.stride, osx=lay.stride,
+                        ory=ph["ry"], orx=ph["rx"], bias=lay.bias_p.data_ptr() if lay.has_bias else None, act=op.act,
+                        out_f32=(out.buf.dt == torch.float32 and self.dtype != torch.float32))
+                    npx = nf * ph["oh"] * ph["ow"]
+                    o.meta = dict(cls="conv_fwd", name=lay.name, flops=2.0 * npx * lay.cout * lay.cin * ph["th"] * ph["tw"],
+                                  bytes=float(self.es * (nf * x.H * x.W * lay.cout + npx * lay.cin)))
+                    self.fwd.append(o)
             elif isinstance(op, FuseOp):
                 out = op.out
                 srcs = [(self.ptr(s), s.buf.C, s.H, s.W) for s in op.srcs]
@@ -708,7 +773,7 @@ class Plan:
         self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
         self._uses_left = {}
         for op in g.ops:
-            if isinstance(op, ConvOp) and op.layer.trainable:
+            if isinstance(op, (ConvOp, ConvTOp)) and op.layer.trainable:
                 self._uses_left[op.layer] = self._uses_left.get(op.layer, 0) + 1
         for key, (region, ch) in g.outputs.items():
             b = region.buf
@@ -773,6 +838,8 @@ class Plan:
                 continue
             if isinstance(op, ConvOp):
                 self._conv_backward(op, gout, gld)
+            elif isinstance(op, ConvTOp):
+                self._convT_backward(op, gout, gld)
             elif isinstance(op, BNOp):
                 x = op.x
                 assert len(x.buf.consumers) == 1, "BatchNorm input must have no other reader"
@@ -914,6 +981,80 @@ class Plan:
                                                          + lay.cout * lay.cin * ph["th"] * ph["tw"])))
                     ops.append(o)
                 return ops
+
+            self._contrib(x, em)
+
+    def _convT_backward(self, op, gout, gld):
+        """nn.ConvTranspose2d backward through its virtual conv (see ConvLayer): the input
+        gradient is that conv run forward over the ConvT output gradient; the weight gradient
+        is that conv's weight gradient with its 'input' = the ConvT output gradient and its
+        'output gradient' = the ConvT input activation; the bias gradient is the column sums
+        of the ConvT output gradient."""
+        lay, x, out = op.layer, op.x, op.out
+        nb = self.nb
+        taps = lay.fwd_taps()
+        ntap = lay.kh * lay.kw
+        if lay.trainable:
+            npix = nb * x.H * x.W
+            tiles = rup(lay.cout_p, 64) // 64 * (rup(out.c, 64) // 64)
+            bkp = 64 if self.dtype == torch.bfloat16 else 32
+            splits = max(1, min(max(1, npix // (bkp * 4)), 1024 // max(1, tiles * ntap)))
+            o = self._op(L.OP_WGRAD)
+            d = o.u.wgrad
+            d.g, d.x, d.ws = self.ptr(x), gout, 0
+            d.g_ld, d.x_ld = x.buf.C, gld
+            d.n, d.oh, d.ow, d.cout = nb, x.H, x.W, lay.cout_p
+            d.ih, d.iw, d.c, d.sy, d.sx = out.H, out.W, out.c, lay.stride, lay.stride
+            d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], 1, 1
+            d.dtype = self.dt
+            lib = L.load()
+            hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))
+            d.splits = hint if hint > 0 else splits
+            slabs = lib.dvie_wgrad_slabs(ctypes.byref(d))
+            self.ws_floats = max(self.ws_floats, slabs * lay.cout_p * ntap * out.c)
+            o.meta = dict(cls="conv_wgrad", name=lay.name, flops=2.0 * npix * lay.cout * lay.cin * ntap,
+                          bytes=float(self.es * (npix * lay.cout + nb * out.H * out.W * lay.cin)))
+            self.bwd.append(o)
+            o = self._op(L.OP_WREDUCE)
+            r = o.u.wreduce
+            r.ws, r.dw, r.cmap = 0, 0, lay.cmap_t.data_ptr()
+            r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, ntap * out.c, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, out.c
+            first = lay not in self.wg_first
+            r.beta = 0 if first else 1
+            self.bwd.append(o)
+            self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
+            if lay.has_bias:
+                opix = nb * out.H * out.W
+                csplits = max(1, min(2048, opix // 512))
+                o = self._op(L.OP_COLSUM)
+                cd = o.u.colsum
+                cd.g, cd.ws, cd.g_ld, cd.rows, cd.c, cd.splits, cd.dtype = gout, 0, gld, opix, out.c, csplits, self.dt
+                self.ws_floats = max(self.ws_floats, csplits * out.c)
+                self.bwd.append(o)
+                o = self._op(L.OP_WREDUCE)
+                r = o.u.wreduce
+                r.ws, r.dw, r.cmap = 0, 0, None
+                r.splits, r.ws_rows, r.ws_k, r.co_off = csplits, out.c, 1, 0
+                r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cin, 1, 1, 1, 1
+                r.beta = 0 if first else 1
+                self.bwd.append(o)
+                self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
+            self.wg_first[lay] = True
+            self._uses_left[lay] -= 1
+            if self._uses_left[lay] == 0:
+                self.completions.append((len(self.bwd), lay))
+        if x.buf.needs_grad:
+            xg = self.ptr(x, grad=True)
+
+            def em(beta, res, res_ld, dact, z, z_ld, lay=lay, x=x, xg=xg, out=out, gout=gout, gld=gld):
+                o = self.conv_desc(gout, gld, nb, out.H, out.W, out.c, lay.wf.data_ptr(), lay.kpad, lay.cout_p,
+                                   x.H, x.W, lay.stride, lay.stride, taps, xg, x.buf.C, x.H, x.W,
+                                   res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)
+                npx = nb * x.H * x.W
+                o.meta = dict(cls="conv_dgrad", name=lay.name, flops=2.0 * npx * lay.cout * lay.cin * ntap,
+                              bytes=float(self.es * (nb * out.H * out.W * lay.cin + npx * lay.cout)))
+                return [o]
 
             self._contrib(x, em)
 

@@ -140,11 +140,18 @@ def _arg(args, name, default):
 class HRNet(FlatParams, nn.Module):
     """Reference: nets/HRNet.py:339-601.  forward(input) -> (rgb, seg_logits)."""
 
+    _stem_extra = 0  # VAEHRNet: channels of the decoded VAE feature in the stem concat
+
     def __init__(self, args):
         super().__init__()
+        self._setup(args)
+        self._build_trunk()
+        self._finish()
+
+    def _setup(self, args):
         self.args = args
         self.highres_large = bool(_arg(args, "highres_large", False))
-        extra = HIGH4_RESOLUTION_NET if self.highres_large else HIGH_RESOLUTION_NET
+        self._extra = HIGH4_RESOLUTION_NET if self.highres_large else HIGH_RESOLUTION_NET
         self.syn_type = _arg(args, "syn_type", "inter")
         self.npo = _arg(args, "num_pred_once", 1) if self.syn_type == "extra" else 1
         self.inpaint_mask = bool(_arg(args, "inpaint_mask", False)) and self.syn_type == "extra"
@@ -159,6 +166,9 @@ class HRNet(FlatParams, nn.Module):
         self.n_frames = 3 if self.fix_init else 2
         self.in_channel = (3 + self.seg_encode_dim) * self.n_frames
 
+    def _build_trunk(self):
+        extra = self._extra
+        self.in_channel += self._stem_extra
         self.seg_encoder = nn.Sequential(
             Conv2d(self.n_classes, 32, 3, 1, 1), nn.ELU(),
             Conv2d(32, 32, 3, 1, 1), nn.ELU(),
@@ -191,7 +201,8 @@ class HRNet(FlatParams, nn.Module):
         self.seg_layer = nn.Sequential(Conv2d(last, last, 1, 1, 0), nn.LeakyReLU(0.2, inplace=False),
                                        Conv2d(last, self.seg_out_dim, 3, 1, 1))
 
-        self.dtype = precision_of(args)
+    def _finish(self):
+        self.dtype = precision_of(self.args)
         self._pool = PlanPool(self._build_plan)
         self._flatten(order=self._backward_order())
 
@@ -249,18 +260,24 @@ class HRNet(FlatParams, nn.Module):
     def _stem_cmap(self):
         """packed stem position -> reference input channel ([rgb(3F), seg_enc(4 each)])."""
         F = self.n_frames
+        e = self._stem_extra  # VAEHRNet: the VAE feature leads the reference concat (l.991-997)
         cm = []
         for k in range(F):
-            cm += [3 * F + 4 * k + i for i in range(4)] + [-1] * 4
-        cm += list(range(3 * F)) + [-1] * (E.rup(3 * F, 8) - 3 * F)
+            cm += [e + 3 * F + 4 * k + i for i in range(4)] + [-1] * 4
+        cm += [e + i for i in range(3 * F)] + [-1] * (E.rup(3 * F, 8) - 3 * F)
+        cm += list(range(e))  # packed last: [segA 0000 segB 0000 rgb 00 | vae]
         return cm
 
-    def _lower(self, g, H, W, dry=False, xgrad=False):
+    def _trunk_params(self):
+        """parameters the HRNet plan writes gradients for"""
+        return self._flat_params
+
+    def _lower(self, g, H, W, dry=False, xgrad=False, vgrad=False):
         A = L
         rup = E.rup
         F = self.n_frames
         segs = []
-        stem_c = 8 * F + rup(3 * F, 8)
+        stem_c = 8 * F + rup(3 * F, 8) + self._stem_extra
         feat = g.buffer("feat", H, W, stem_c)
         for k in range(F):
             s_in = g.buffer(f"seg{k}_in", H, W, 24)
@@ -272,6 +289,9 @@ class HRNet(FlatParams, nn.Module):
             g.conv(E.R(e2), self.seg_encoder[4], E.R(feat, 8 * k, 8), name="seg_encoder.4")
         # xgrad: the frames input needs a gradient (ExtraTrainer rollout feeds a prediction back)
         g.input_nchw(E.R(feat, 8 * F, rup(3 * F, 8)), "x", ext_c=3 * F, requires_grad=xgrad)
+        if self._stem_extra:  # decoded VAE feature (its gradient feeds the decoder backward)
+            g.input_nchw(E.R(feat, 8 * F + rup(3 * F, 8), self._stem_extra), "vae", ext_c=self._stem_extra,
+                         requires_grad=vgrad)
         s1 = g.buffer("stem1", H, W, 64)
         g.conv(E.R(feat), self.conv1, E.R(s1), act=A.ACT_LRELU, cmap=self._stem_cmap(), name="conv1")
         s2 = g.buffer("stem2", H, W, 64)
@@ -422,7 +442,7 @@ class HRNet(FlatParams, nn.Module):
 
     def _build_plan(self, key):
         n, H, W, dtype, train, dev, xgrad = key
-        g = self._lower(E.Graph(dtype), H, W, xgrad=xgrad)
+        g = self._lower(E.Graph(dtype), H, W, xgrad=xgrad, vgrad=bool(train))
         return g.compile(n, dev, backward=train)
 
     def _on_moved(self):
@@ -430,13 +450,15 @@ class HRNet(FlatParams, nn.Module):
 
     # ---- execution ----
     def run_forward(self, inputs, train):
-        x, seg = inputs
+        x, seg = inputs[:2]
         n, _, H, W = x.shape
         L.require_gpu(x)
         xgrad = bool(train) and bool(getattr(self, "_in_needs", (False,))[0])
         plan = self._pool.acquire((n, H, W, self.dtype, bool(train), x.device, xgrad))
         plan.set_input("x", x)
         plan.set_input("seg", seg)
+        if len(inputs) > 2:
+            plan.set_input("vae", inputs[2])
         rgb = torch.empty((n, H, W, E.rup(self.rgb_out_dim, 8)), dtype=torch.float32, device=x.device)
         segout = torch.empty((n, H, W, E.rup(self.seg_out_dim, 8)), dtype=torch.float32, device=x.device)
         plan.set_output("rgb", rgb)
@@ -471,7 +493,7 @@ class HRNet(FlatParams, nn.Module):
         return cuts, ranges
 
     def run_backward(self, plan, inputs, grads, needs):
-        accumulate = self.grad_views()
+        accumulate = self.grad_views(self._trunk_params())
         plan.set_param_grads(accumulate)
         g_rgb, g_seg = grads
         if E.DEBUG_NAN:
@@ -479,10 +501,13 @@ class HRNet(FlatParams, nn.Module):
                   f"seg {bool(torch.isfinite(g_seg).all())}", flush=True)
         plan.set_output_grad("rgb", g_rgb.float())
         plan.set_output_grad("segout", g_seg.float())
-        gx = None
+        gx = gv = None
         if "x" in plan.ext_grad:
             gx = torch.empty(inputs[0].shape, dtype=torch.float32, device=inputs[0].device)
             plan.set_input_grad("x", gx)
+        if "vae" in plan.ext_grad:
+            gv = torch.empty(inputs[2].shape, dtype=torch.float32, device=inputs[2].device)
+            plan.set_input_grad("vae", gv)
         hook = self.grad_hook
         if hook is None:
             plan.run_backward()
@@ -490,7 +515,7 @@ class HRNet(FlatParams, nn.Module):
             cuts, ranges = self._buckets(plan, hook[0])
             plan.run_backward(cuts=cuts, on_cut=lambda k: hook[1](*ranges[k]))
             hook[1](*ranges[-1])
-        return [gx, None]
+        return [gx, None] + ([gv] if len(inputs) > 2 else [])
 
     def forward_split(self, x, seg):
         """x: (B, 3F, H, W) frames in [-1, 1]; seg: (B, 20F, H, W) one-hot segmentations."""

@@ -2,6 +2,7 @@
 from .conv import Conv2d
 from .ExtraNet import ExtraNet
 from .HRNet import HRNet
+from .VAEHRNet import VAEHRNet
 from .InterNet import InterNet
 from .vgg import VGG19, my_vgg, vgg19_features
 from .disc import (FrameDiscriminator, FrameLocalDiscriminator, FrameSNDiscriminator, FrameSNLocalDiscriminator,

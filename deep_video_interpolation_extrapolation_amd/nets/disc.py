@@ -105,6 +105,76 @@ def _packing(widths):
     return slices, cmap, off
 
 
+def lower_sequential(g, mods, x, prefix, trainable, cmap=None, out_key=None, head_c=None):
+    """Lower an nn.Sequential of Conv2d / SpectralNorm(Conv2d) / ConvTranspose2d (each with
+    an optional BatchNorm2d and LeakyReLU after it), ResnetBlock / ResnetSNBlock and a final
+    AvgPool2d (head "score", head_c channels) into the engine graph `g`, starting from region
+    `x`.  Buffers are named f"{prefix}.{i}" after the Sequential index (the activation names
+    the oracles use).  A conv with nothing after it writes the external fp32 output
+    `out_key`.  Returns the last region (None after an external output or a head)."""
+    A = L
+    i, first = 0, True
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, (nn.Conv2d, SpectralNorm, nn.ConvTranspose2d)):
+            conv = _conv_of(m)
+            tr = isinstance(conv, nn.ConvTranspose2d)
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            if tr:
+                hh, ww = (x.H - 1) * s - 2 * p + k, (x.W - 1) * s - 2 * p + k
+            else:
+                hh, ww = (x.H + 2 * p - k) // s + 1, (x.W + 2 * p - k) // s + 1
+            cm = cmap if first else None
+            first = False
+            name = f"{prefix}.{i}"
+
+            def emit(src, dst, act, conv=conv, cm=cm, name=name, tr=tr):
+                if tr:
+                    assert cm is None, "a transposed conv cannot take a packed input map"
+                    g.convT(src, conv, dst, act=act, trainable=trainable, name=name)
+                else:
+                    g.conv(src, conv, dst, act=act, cmap=cm, trainable=trainable, name=name)
+
+            if nxt is None:  # the map is the output
+                assert out_key is not None and not tr
+                o = g.buffer(out_key, hh, ww, E.rup(conv.out_channels, 8), dtype=torch.float32, external=True)
+                emit(x, E.R(o), A.ACT_NONE)
+                g.output(out_key, E.R(o), conv.out_channels)
+                return None
+            if isinstance(nxt, nn.BatchNorm2d):
+                act = A.ACT_LRELU if i + 2 < len(mods) and isinstance(mods[i + 2], nn.LeakyReLU) else A.ACT_NONE
+                t = g.buffer(name, hh, ww, E.rup(conv.out_channels, 8))
+                emit(x, E.R(t), A.ACT_NONE)
+                o = g.buffer(f"{prefix}.{i + 1}", hh, ww, E.rup(conv.out_channels, 8))
+                g.bn(E.R(t), nxt, E.R(o), act=act, trainable=trainable)
+                x = E.R(o)
+                i += 3 if act == A.ACT_LRELU else 2
+                continue
+            act = A.ACT_LRELU if isinstance(nxt, nn.LeakyReLU) else A.ACT_NONE
+            o = g.buffer(name, hh, ww, E.rup(conv.out_channels, 8))
+            emit(x, E.R(o), act)
+            x = E.R(o)
+            i += 2 if act == A.ACT_LRELU else 1
+            continue
+        if isinstance(m, (ResnetBlock, ResnetSNBlock)):
+            c0, c2 = _conv_of(m.conv[0]), _conv_of(m.conv[2])
+            h = g.buffer(f"{prefix}.{i}.h", x.H, x.W, E.rup(c0.out_channels, 8))
+            g.conv(x, c0, E.R(h), act=A.ACT_LRELU, trainable=trainable, name=f"{prefix}.{i}.conv.0")
+            o = g.buffer(f"{prefix}.{i}.out", x.H, x.W, E.rup(c2.out_channels, 8))
+            g.conv(E.R(h), c2, E.R(o), res=x, trainable=trainable, name=f"{prefix}.{i}.conv.2")
+            x = E.R(o)
+            i += 1
+            continue
+        if isinstance(m, nn.AvgPool2d):
+            k = m.kernel_size if isinstance(m.kernel_size, int) else m.kernel_size[0]
+            assert head_c is not None and x.c == head_c
+            g.head(x, k, "score")
+            return None
+        raise TypeError(f"unsupported layer {prefix}.{i}: {m}")
+    return x
+
+
 class _PlanDiscriminator(FlatParams, nn.Module):
     """Shared plan lowering / autograd plumbing of the discriminators."""
 
@@ -127,56 +197,9 @@ class _PlanDiscriminator(FlatParams, nn.Module):
         inp = g.buffer("disc_in", H, W, total)
         for k, (c0, c, w) in enumerate(slices):
             g.input_nchw(E.R(inp, c0, c), f"in{k}", ext_c=w, requires_grad=bool(in_grads[k]))
-        x = E.R(inp)
-        mods = list(self.layer)
-        i, first = 0, True
-        while i < len(mods):
-            m = mods[i]
-            if isinstance(m, (nn.Conv2d, SpectralNorm)):
-                conv = _conv_of(m)
-                nxt = mods[i + 1] if i + 1 < len(mods) else None
-                hh = (x.H + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
-                ww = (x.W + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
-                cm = cmap if first else None
-                first = False
-                if nxt is None:  # local variants: the map is the output
-                    assert self.local
-                    o = g.buffer("score", hh, ww, E.rup(conv.out_channels, 8), dtype=torch.float32, external=True)
-                    g.conv(x, conv, E.R(o), cmap=cm, trainable=trainable, name=f"layer.{i}")
-                    g.output("score", E.R(o), conv.out_channels)
-                    i += 1
-                    continue
-                if isinstance(nxt, nn.BatchNorm2d):
-                    act = A.ACT_LRELU if i + 2 < len(mods) and isinstance(mods[i + 2], nn.LeakyReLU) else A.ACT_NONE
-                    t = g.buffer(f"layer.{i}", hh, ww, E.rup(conv.out_channels, 8))
-                    g.conv(x, conv, E.R(t), cmap=cm, trainable=trainable, name=f"layer.{i}")
-                    o = g.buffer(f"layer.{i + 1}", hh, ww, E.rup(conv.out_channels, 8))
-                    g.bn(E.R(t), nxt, E.R(o), act=act, trainable=trainable)
-                    x = E.R(o)
-                    i += 3 if act == A.ACT_LRELU else 2
-                    continue
-                act = A.ACT_LRELU if isinstance(nxt, nn.LeakyReLU) else A.ACT_NONE
-                o = g.buffer(f"layer.{i}", hh, ww, E.rup(conv.out_channels, 8))
-                g.conv(x, conv, E.R(o), act=act, cmap=cm, trainable=trainable, name=f"layer.{i}")
-                x = E.R(o)
-                i += 2 if act == A.ACT_LRELU else 1
-                continue
-            if isinstance(m, (ResnetBlock, ResnetSNBlock)):
-                c0, c2 = _conv_of(m.conv[0]), _conv_of(m.conv[2])
-                h = g.buffer(f"layer.{i}.h", x.H, x.W, E.rup(c0.out_channels, 8))
-                g.conv(x, c0, E.R(h), act=A.ACT_LRELU, trainable=trainable, name=f"layer.{i}.conv.0")
-                o = g.buffer(f"layer.{i}.out", x.H, x.W, E.rup(c2.out_channels, 8))
-                g.conv(E.R(h), c2, E.R(o), res=x, trainable=trainable, name=f"layer.{i}.conv.2")
-                x = E.R(o)
-                i += 1
-                continue
-            if isinstance(m, nn.AvgPool2d):
-                k = m.kernel_size if isinstance(m.kernel_size, int) else m.kernel_size[0]
-                assert x.c == self.out_c
-                g.head(x, k, "score")
-                i += 1
-                continue
-            raise TypeError(f"unsupported discriminator layer {i}: {m}")
+        assert self.local or self.out_c is not None
+        lower_sequential(g, list(self.layer), E.R(inp), "layer", trainable, cmap=cmap,
+                         out_key="score" if self.local else None, head_c=None if self.local else self.out_c)
         return g
 
     def _build_plan(self, key):

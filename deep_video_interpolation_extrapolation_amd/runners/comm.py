@@ -38,8 +38,10 @@ class GradSync:
         # owners that launch their buckets from inside their backward (HRNet); the others
         # (discriminators, a few MB, gradients accumulated over two plan backwards) get one
         # all-reduce of their flat gradient after the backward
-        self.hooked = [m for m in self.flat_owners if hasattr(m, "_buckets")]
-        self.post = [m for m in self.flat_owners if not hasattr(m, "_buckets")]
+        # (VAEHRNet: parameters of several chained plans share one flat buffer, so it syncs
+        # after its whole backward)
+        self.hooked = [m for m in self.flat_owners if hasattr(m, "_buckets") and not getattr(m, "post_sync", False)]
+        self.post = [m for m in self.flat_owners if m not in self.hooked]
         self.works = []
         if self.W > 1:
             for m in self.flat_owners:  # DDP's initial parameter broadcast

@@ -67,13 +67,17 @@ class FlatParams:
             self._flat_grad = torch.zeros_like(self._flat)
         return self._flat_grad
 
-    def grad_views(self):
-        """Attach .grad of every parameter to its view of the flat gradient buffer.
-        Returns True if the parameters already had gradients (accumulate mode)."""
+    def grad_views(self, params=None):
+        """Attach .grad of every parameter (or of the subset `params`: the ones one plan
+        writes, when several plans share the flat buffer) to its view of the flat gradient
+        buffer.  Returns True if those parameters already had gradients (accumulate mode)."""
         fg = self.flat_grad()
         accumulate = False
+        sel = None if params is None else {id(p) for p in params}
         for p, (off, n, shape) in zip(self._flat_params, self._flat_specs):
             if not p.requires_grad:  # frozen (e.g. SpectralNorm u, v): .grad stays None
+                continue
+            if sel is not None and id(p) not in sel:
                 continue
             if p.grad is None:
                 p.grad = fg[off:off + n].view(shape)

@@ -413,6 +413,16 @@ int dvie_sn_fwd(const dvie_sn_layer* layers, int n, float* state, void* stream);
 int dvie_sn_bwd(const dvie_sn_layer* layers, int n, const float* state, void* stream);
 
 /*
+ * VAEHRNet reparameterisation (reference nets/HRNet.py:960-966), fp32, n elements:
+ *   forward  z = eps * exp(0.5 * logvar) + mu
+ *   backward gmu (+)= gz; glogvar (+)= gz * eps * 0.5 * exp(0.5 * logvar)   (beta: accumulate)
+ * eps is the caller's standard-normal draw (std.new(std.size()).normal_()).
+ */
+int dvie_reparam_fwd(const float* mu, const float* logvar, const float* eps, float* z, long long n, void* stream);
+int dvie_reparam_bwd(const float* logvar, const float* eps, const float* gz, float* gmu, float* glogvar, long long n,
+                     int beta, void* stream);
+
+/*
  * Op-list executor: runs n descriptors in order on one stream with a single host call
  * (the per-step forward and backward plans of the HRNet / VGG executors).
  */

@@ -13,8 +13,9 @@ import torch.nn.functional as F
 STAGES = {False: [[64, 128], [64, 128, 256]], True: [[64, 128], [64, 128, 256], [64, 128, 256, 512]]}
 
 
-def conv_specs(n_frames=2, rgb_out=3, seg_out=20, large=False):
-    """[(name, cin, cout, k, stride, pad, bias)] in reference construction order."""
+def conv_specs(n_frames=2, rgb_out=3, seg_out=20, large=False, extra_in=0):
+    """[(name, cin, cout, k, stride, pad, bias)] in reference construction order
+    (extra_in: VAEHRNet's decoded feature channels in the stem concat, HRNet.py:718-720)."""
     S = []
 
     def add(name, cin, cout, k, s=1, p=None, bias=False):
@@ -25,7 +26,7 @@ def conv_specs(n_frames=2, rgb_out=3, seg_out=20, large=False):
     add("seg_encoder.2", 32, 32, 3, bias=True)
     add("seg_encoder.4", 32, 4, 3, bias=True)
     # stem (l.367-371)
-    add("conv1", 7 * n_frames, 64, 3, bias=True)
+    add("conv1", 7 * n_frames + extra_in, 64, 3, bias=True)
     add("conv2", 64, 64, 3, bias=True)
     # layer1: _make_layer builds the downsample before the first Bottleneck (l.479-495)
     add("layer1.0.downsample.0", 64, 256, 1)
@@ -66,10 +67,12 @@ def conv_specs(n_frames=2, rgb_out=3, seg_out=20, large=False):
     return S
 
 
-def init_params(seed=1024, **kw):
-    """State dict with the reference's seeded nn.Conv2d initialisation."""
-    torch.manual_seed(seed)
-    sd = {}
+def init_params(seed=1024, sd=None, **kw):
+    """State dict with the reference's seeded nn.Conv2d initialisation (seed None: continue
+    the current RNG stream, adding to `sd`)."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    sd = {} if sd is None else sd
     for name, cin, cout, k, s, p, bias in conv_specs(**kw):
         m = nn.Conv2d(cin, cout, k, s, p, bias=bias)
         sd[name + ".weight"] = m.weight.detach().clone()
@@ -88,9 +91,10 @@ def _lrelu(x):
     return F.leaky_relu(x, 0.2)
 
 
-def forward(P, inp, n_frames=2, large=False, taps=None):
+def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
     """HRNet.forward (nets/HRNet.py:524-601) for syn_type 'inter' (and 'extra' without
-    inpainting).  inp: (B, 3F + 20F, H, W).  Returns (rgb, seg_logits)."""
+    inpainting).  inp: (B, 3F + 20F, H, W).  Returns (rgb, seg_logits).  pre: VAEHRNet's
+    decoded feature, leading the stem concat (HRNet.py:997)."""
     F_ = n_frames
     segs = [inp[:, 3 * F_ + 20 * k: 3 * F_ + 20 * (k + 1)] for k in range(F_)]
     enc = []
@@ -98,7 +102,7 @@ def forward(P, inp, n_frames=2, large=False, taps=None):
         h = F.elu(_conv(P, "seg_encoder.0", s))
         h = F.elu(_conv(P, "seg_encoder.2", h))
         enc.append(_conv(P, "seg_encoder.4", h))
-    x = torch.cat([inp[:, :3 * F_]] + enc, 1)
+    x = torch.cat(([pre] if pre is not None else []) + [inp[:, :3 * F_]] + enc, 1)
     x = _lrelu(_conv(P, "conv1", x))
     x = _lrelu(_conv(P, "conv2", x))
     for b in range(4):  # Bottleneck (l.66-85)

@@ -100,3 +100,22 @@ def sepunet_inputs(n=2, H=32, W=64, seed=41):
     g_rgb = torch.randn((n, 3, H, W), generator=g)
     g_seg = torch.randn((n, 20, H, W), generator=g)
     return torch.cat([x, seg], 1), mask, g_rgb, g_seg
+
+
+def vae_inputs(n=2, H=128, W=128, seed=61):
+    """VAEHRNet: frames / segs (hrnet_input), gt frame + one-hot seg, and upstream gradients of
+    (rgb, seg, mu, logvar)."""
+    x, seg = hrnet_input(n, H, W)
+    g = _gen(seed)
+    gt_x = torch.rand((n, 3, H, W), generator=g) * 2 - 1
+    gt_seg = onehot(torch.randint(0, 20, (n, H, W), generator=g))
+    grads = (torch.randn((n, 3, H, W), generator=g), torch.randn((n, 20, H, W), generator=g),
+             torch.randn((n, 1024), generator=g), torch.randn((n, 1024), generator=g))
+    return x, seg, gt_x, gt_seg, grads
+
+
+def vae_eps(n=2, seed=77):
+    """the reparameterisation noise the reference draws right after torch.manual_seed(seed)
+    (std.new(std.size()).normal_(), nets/HRNet.py:963)"""
+    torch.manual_seed(seed)
+    return torch.empty(n, 1024).normal_()

@@ -19,6 +19,8 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
   sepunet.npz    G7: reference SepUNet (train-mode BatchNorm, align_corners=True upsampling,
                      tanh head) at 32x64: outputs, input-gradient stats, parameter-gradient
                      stats, running statistics
+  vaehrnet.npz   G9: reference VAEHRNet (train mode, 128x128): rgb / seg stats + samples, mu,
+                     logvar, parameter-gradient stats, initial-weight checksums, running stats
   step.npz       G4: one training step of the reference modules (InterTrainer.py:380-441
                      body): loss dict, per-parameter gradient stats, post-Adamax checksums
 """
@@ -250,9 +252,37 @@ def g8():
     np.savez_compressed(os.path.join(HERE, "disc_sn.npz"), **out)
 
 
+def g9():
+    """reference VAEHRNet (train mode, 128x128 - its only working size) forward + backward:
+    the reparameterisation noise is the CPU draw right after torch.manual_seed(77)"""
+    torch.manual_seed(1024)
+    m = ref_nets.VAEHRNet(args_ns())
+    m.train()
+    x, seg, gt_x, gt_seg, (g_rgb, g_seg, g_mu, g_lv) = inputs.vae_inputs()
+    torch.manual_seed(77)
+    rgb, segout, mu, logvar = m(torch.cat([x, seg], 1), gt_x, gt_seg)
+    ((rgb * g_rgb).sum() + (segout * g_seg).sum() + (mu * g_mu).sum() + (logvar * g_lv).sum()).backward()
+    out = {"mu": mu.detach().numpy(), "logvar": logvar.detach().numpy()}
+    for k, t in (("rgb", rgb), ("seg", segout)):
+        v = t.detach().double().reshape(-1)
+        out[k] = np.concatenate([[float(v.sum()), float(v.abs().sum()), float(v.norm())],
+                                 v[inputs.sample_idx(v.numel())].numpy()])
+    named = dict(m.named_parameters())
+    names = sorted(named)
+    out["param_names"] = np.array(names)
+    out["grad_stats"] = np.array([[float(named[n].grad.double().sum()), float((named[n].grad.double() ** 2).sum())]
+                                  for n in names])
+    _, cs = checksums({n: p.detach() for n, p in named.items()})
+    out["param_checksums"] = cs
+    bufs = {k: v for k, v in m.state_dict().items() if "running" in k}
+    out["buf_names"] = np.array(sorted(bufs))
+    out["bufs"] = np.concatenate([bufs[k].numpy().reshape(-1) for k in sorted(bufs)])
+    np.savez_compressed(os.path.join(HERE, "vaehrnet.npz"), **out)
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()
