@@ -241,3 +241,36 @@ def test_intergan_step_matches_oracle(dev):
             total += dw.numel()
         assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (tag, float(np.median(errs)), max(errs))
         assert moved <= 1e-3 * total, (tag, moved, total)
+
+
+def test_intergan_vae_sn_two_steps(dev):
+    """The reference's InterGAN configuration: VAEHRNet coarse model (KLD term) with the SN
+    frame / video discriminators at 128x128, two fp32 steps: the second runs with SpectralNorm
+    u / v trainable after set_net_grad(True) (per-parameter Adam step counts); losses stay
+    finite, the KLD term sits after the CE term as in the reference (InterGANTrainer.py:406-409)
+    and u moves with the power iteration."""
+    os.environ["DVIE_PRECISION"] = "fp32"
+    from deep_video_interpolation_extrapolation_amd.options import default_args
+    from deep_video_interpolation_extrapolation_amd.runners.InterGANTrainer import InterGANTrainer
+    args = default_args("INTER", syn_type="inter", model="InterGANNet", gan=True, train_coarse=True, frame_disc=True,
+                        video_disc=True, train_frame_disc=True, train_video_disc=True, seg_disc=True,
+                        coarse_model="VAEHRNet", vae=True, frame_disc_model="FrameSNDiscriminator",
+                        video_disc_model="VideoSNDiscriminator", batch_size=2, input_h=128, input_w=128,
+                        precision="fp32", synthetic=2, num_workers=0, split="train")
+    torch.manual_seed(1024)
+    tr = InterGANTrainer(args)
+    m = tr.model.module
+    sn0 = m.frame_disc_model.layer[0].module
+    u0 = sn0.weight_u.detach().clone()
+    data = inputs.step_batch(2, 128, 128)
+    ld1 = tr.step(data)
+    assert sn0.weight_u.requires_grad  # set_net_grad(True) after the G pass, as the reference
+    ld2 = tr.step(data)
+    torch.cuda.synchronize()
+    keys = list(ld1.keys())
+    assert keys.index("coarse_kld_loss") == keys.index("coarse_ce_loss") + 1, keys
+    assert keys[-1] == "loss_all" and list(ld2.keys()) == keys
+    for ld in (ld1, ld2):
+        assert all(np.isfinite(float(v)) for v in ld.values()), ld
+    assert not torch.equal(sn0.weight_u.detach(), u0)
+    assert sn0.weight_u.grad is not None and bool(torch.isfinite(sn0.weight_u.grad).all())
