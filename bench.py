@@ -77,36 +77,54 @@ def cpu_baseline(H, W):
 
 def warp_roofline(dev, n, H, W, reps=20):
     """The optical-flow warp (FlowWrapper, utils/net_utils.py:89-114; dormant in the
-    InterNet step) on (n, 3, H, W) frames: forward and backward timed with HIP events on the
-    launch stream, against the HBM roofline.  Algorithmic bytes per pixel (fp32): forward
-    img 12 + flow 8 + out 12 = 32; backward img 12 + flow 8 + dout 12 + dimg 12 + dflow 8 = 52."""
-    from deep_video_interpolation_extrapolation_amd.utils.net_utils import flow_warp
+    InterNet step) on (n, 3, H, W) frames: dvie_warp_fwd / dvie_warp_bwd launched back to back
+    through the C ABI (no autograd or allocation between launches), timed with HIP events on
+    the launch stream, against the HBM roofline.  Algorithmic bytes per pixel (fp32):
+    forward img 12 + flow 8 + out 12 = 32; backward img 12 + flow 8 + dout 12 + dimg 12 +
+    dflow 8 = 52 (the dimg zero-fill the backward accumulates into is timed with it)."""
+    import ctypes
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    lib = L.load()
     g = torch.Generator(device=dev).manual_seed(5)
-    x = torch.rand((n, 3, H, W), generator=g, device=dev).requires_grad_(True)
-    flow = ((torch.rand((n, 2, H, W), generator=g, device=dev) * 2 - 1) * 0.05).requires_grad_(True)
+    x = torch.rand((n, 3, H, W), generator=g, device=dev)
+    # smooth optical-flow-like field: up to ~4 px at 256x512 (the same normalised field at
+    # other sizes) plus 0.1 px noise; per-pixel random flow is a gather/scatter stress test,
+    # not optical flow
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H, device=dev), torch.linspace(0, 1, W, device=dev), indexing="ij")
+    flow = torch.stack([torch.sin(6.3 * xx + 3.1 * yy) * 0.016, torch.cos(4.7 * yy - 2.9 * xx) * 0.024])
+    flow = flow.unsqueeze(0).repeat(n, 1, 1, 1) + (torch.rand((n, 2, H, W), generator=g, device=dev) - 0.5) * 4e-4
     go = torch.randn((n, 3, H, W), generator=g, device=dev)
-    for _ in range(3):
-        flow_warp(x, flow).backward(go)
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    tf = tb = 0.0
-    for _ in range(reps):
-        x.grad = flow.grad = None
-        ev[0].record()
-        y = flow_warp(x, flow)
-        ev[1].record()
-        y.backward(go)
-        ev[2].record()
+    out, dx, dflow = torch.empty_like(x), torch.zeros_like(x), torch.empty_like(flow)
+    d = L.WarpDesc()
+    d.img, d.flow, d.out, d.dout, d.dimg, d.dflow = (t.data_ptr() for t in (x, flow, out, go, dx, dflow))
+    d.n, d.c, d.h, d.w, d.align_corners = n, 3, H, W, 1
+    ws = torch.empty(lib.dvie_warp_ws_floats(ctypes.byref(d)), dtype=torch.float32, device=dev)
+    d.ws = ws.data_ptr()
+    s = L.stream_ptr(dev)
+
+    def fwd():
+        L.check(lib.dvie_warp_fwd(ctypes.byref(d), s), "warp fwd")
+
+    def bwd():
+        dx.zero_()
+        L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), "warp bwd")
+
+    res = {}
+    for tag, fn, bpp in (("fwd", fwd, 32.0), ("bwd", bwd, 52.0)):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
         torch.cuda.synchronize()
-        tf += ev[0].elapsed_time(ev[1])
-        tb += ev[1].elapsed_time(ev[2])
-    px = n * H * W
-    fwd = 32.0 * px / (tf / reps * 1e-3) / 1e9
-    bwd = 52.0 * px / (tb / reps * 1e-3) / 1e9
-    return {"shape": [n, 3, H, W], "fwd_ms": round(tf / reps, 4), "bwd_ms": round(tb / reps, 4),
-            "fwd_GBps": round(fwd, 1), "bwd_GBps": round(bwd, 1), "fwd_frac": round(fwd / PEAK_HBM_GBS, 4),
-            "bwd_frac": round(bwd / PEAK_HBM_GBS, 4), "bytes_per_px": {"fwd": 32, "bwd": 52},
-            "note": "bwd includes the zero-fill of dimg (torch.zeros) that its atomics accumulate into"}
+        ms = e0.elapsed_time(e1) / reps
+        gbs = bpp * n * H * W / (ms * 1e-3) / 1e9
+        res[tag + "_ms"], res[tag + "_GBps"], res[tag + "_frac"] = round(ms, 4), round(gbs, 1), round(gbs / PEAK_HBM_GBS, 4)
+    res.update(shape=[n, 3, H, W], bytes_per_px={"fwd": 32, "bwd": 52},
+               flow="smooth, |dx| <= %.1f px, |dy| <= %.1f px" % (0.016 * (W - 1) / 2, 0.024 * (H - 1) / 2))
+    return res
 
 
 def main():
@@ -233,6 +251,7 @@ def main():
             "step_breakdown_ms": {k: round(v["ms"] / max(1, a.profile_steps), 3) for k, v in sorted(agg.items())},
         }
         out["warp"] = warp_roofline(dev, a.batch, a.height, a.width)
+        out["warp_1024x2048"] = warp_roofline(dev, a.batch, 1024, 2048, reps=5)  # BASELINE configs[4] frames
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.height, a.width)
         else:

@@ -108,7 +108,7 @@ class LossDesc(ctypes.Structure):
 
 class WarpDesc(ctypes.Structure):
     _fields_ = [
-        ("img", vp), ("flow", vp), ("out", vp), ("dout", vp), ("dimg", vp), ("dflow", vp),
+        ("img", vp), ("flow", vp), ("out", vp), ("dout", vp), ("dimg", vp), ("dflow", vp), ("ws", vp),
         ("n", i32), ("c", i32), ("h", i32), ("w", i32),
         ("align_corners", i32), ("pad0", i32),
     ]
@@ -176,7 +176,7 @@ EXPORTS = [
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
-    "dvie_reparam_bwd",
+    "dvie_reparam_bwd", "dvie_warp_ws_floats",
 ]
 
 _lib = None
@@ -220,6 +220,8 @@ def load():
         lib.dvie_run_ops.argtypes = [vp, i32, vp]
         lib.dvie_loss_partial_count.argtypes = [vp]
         lib.dvie_loss_partial_count.restype = ctypes.c_size_t
+        lib.dvie_warp_ws_floats.argtypes = [vp]
+        lib.dvie_warp_ws_floats.restype = ctypes.c_size_t
         lib.dvie_loss_ws_floats.argtypes = [vp]
         lib.dvie_loss_ws_floats.restype = ctypes.c_size_t
         lib.dvie_adamax.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]

@@ -265,8 +265,11 @@ size_t dvie_loss_ws_floats(const dvie_loss_desc* d);
  * zeros padding, align_corners=True as in the pinned torch 1.0.1):
  *   gx = linspace(-1,1,W)[x] - flow[n,0,y,x],  gy = linspace(-1,1,H)[y] - flow[n,1,y,x]
  *   out[n,c,y,x] = bilinear(img[n,c], (gx+1)/2*(W-1), (gy+1)/2*(H-1))
- * fp32, NCHW contiguous.  Backward: dimg (accumulated with atomics — zero it first) and
- * dflow (overwritten), given dout.
+ * fp32, NCHW contiguous.  Backward: dimg (accumulated — zero it first) and dflow
+ * (overwritten), given dout.  With a workspace `ws` of dvie_warp_ws_floats(d) floats the
+ * image gradient is aggregated per tile in LDS and written through per-tile partial regions
+ * summed by a second gather pass (only samples that land outside their tile's region use
+ * global atomics); ws = NULL: one global atomic per bilinear corner.
  */
 typedef struct dvie_warp_desc {
   const float* img;
@@ -275,12 +278,14 @@ typedef struct dvie_warp_desc {
   const float* dout;
   float* dimg;
   float* dflow;
+  float* ws;
   int n, c, h, w;
   int align_corners, pad0;
 } dvie_warp_desc;
 
 int dvie_warp_fwd(const dvie_warp_desc* d, void* stream);
 int dvie_warp_bwd(const dvie_warp_desc* d, void* stream);
+size_t dvie_warp_ws_floats(const dvie_warp_desc* d);
 
 /*
  * Fused Adamax step over a flat fp32 buffer (torch.optim.Adamax semantics,

@@ -145,6 +145,47 @@ def test_warp(dev):
     assert float((fg.grad.cpu() - fr.grad).abs().max()) < 1e-3
 
 
+@pytest.mark.parametrize("tiled", [True, False])
+@pytest.mark.parametrize("shape", [(2, 5, 40, 136), (1, 3, 33, 66)])
+def test_warp_multi_tile(dev, tiled, shape):
+    """dvie_warp_bwd through the C ABI on frames spanning many 64x16 tiles: a smooth flow of
+    a few pixels (samples that cross tile borders but stay in the LDS region) plus a sparse
+    set of large displacements (the far-sample atomics), both backward variants; 5 channels
+    exercise the partial channel block.  Tolerances: out 1e-5, dimg 1e-4, dflow 1e-3 abs."""
+    import ctypes
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    n, c, h, w = shape
+    g = torch.Generator().manual_seed(23)
+    x = torch.rand((n, c, h, w), generator=g)
+    yy, xx = torch.meshgrid(torch.arange(h, dtype=torch.float32), torch.arange(w, dtype=torch.float32), indexing="ij")
+    flow = torch.stack([torch.sin(xx / 9.0 + yy / 13.0) * 6.0 / w, torch.cos(yy / 7.0 - xx / 17.0) * 5.0 / h])
+    flow = flow.unsqueeze(0).repeat(n, 1, 1, 1) + (torch.rand((n, 2, h, w), generator=g) - 0.5) * 0.02
+    far = torch.rand((n, 1, h, w), generator=g) < 0.05
+    flow = torch.where(far, (torch.rand((n, 2, h, w), generator=g) * 2 - 1) * 0.8, flow)
+    dout = torch.randn((n, c, h, w), generator=g)
+    xr, fr = x.clone().requires_grad_(True), flow.clone().requires_grad_(True)
+    yr = OW.flow_warp(xr, fr)
+    yr.backward(dout)
+
+    lib = L.load()
+    xd, fd, gd = x.to(dev), flow.to(dev), dout.to(dev)
+    out, dx, dfl = torch.empty_like(xd), torch.zeros_like(xd), torch.empty_like(fd)
+    d = L.WarpDesc()
+    d.img, d.flow, d.out, d.dout, d.dimg, d.dflow = (t.data_ptr() for t in (xd, fd, out, gd, dx, dfl))
+    d.n, d.c, d.h, d.w, d.align_corners = n, c, h, w, 1
+    ws = None
+    if tiled:
+        ws = torch.empty(lib.dvie_warp_ws_floats(ctypes.byref(d)), dtype=torch.float32, device=dev)
+        d.ws = ws.data_ptr()
+    s = L.stream_ptr(dev)
+    L.check(lib.dvie_warp_fwd(ctypes.byref(d), s), "warp fwd")
+    L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), "warp bwd")
+    torch.cuda.synchronize()
+    assert float((out.cpu() - yr.detach()).abs().max()) < 1e-5
+    assert float((dx.cpu() - xr.grad).abs().max()) < 1e-4
+    assert float((dfl.cpu() - fr.grad).abs().max()) < 1e-3
+
+
 def _hrnet(dev, prec, monkeypatch):
     monkeypatch.setenv("DVIE_PRECISION", prec)
     import types
