@@ -81,7 +81,7 @@ def warp_roofline(dev, n, H, W, reps=20):
     through the C ABI (no autograd or allocation between launches), timed with HIP events on
     the launch stream, against the HBM roofline.  Algorithmic bytes per pixel (fp32):
     forward img 12 + flow 8 + out 12 = 32; backward img 12 + flow 8 + dout 12 + dimg 12 +
-    dflow 8 = 52 (the dimg zero-fill the backward accumulates into is timed with it)."""
+    dflow 8 = 52 (dimg is overwritten: no zero-fill)."""
     import ctypes
     from deep_video_interpolation_extrapolation_amd import _lib as L
     lib = L.load()
@@ -98,15 +98,12 @@ def warp_roofline(dev, n, H, W, reps=20):
     d = L.WarpDesc()
     d.img, d.flow, d.out, d.dout, d.dimg, d.dflow = (t.data_ptr() for t in (x, flow, out, go, dx, dflow))
     d.n, d.c, d.h, d.w, d.align_corners = n, 3, H, W, 1
-    ws = torch.empty(lib.dvie_warp_ws_floats(ctypes.byref(d)), dtype=torch.float32, device=dev)
-    d.ws = ws.data_ptr()
     s = L.stream_ptr(dev)
 
     def fwd():
         L.check(lib.dvie_warp_fwd(ctypes.byref(d), s), "warp fwd")
 
     def bwd():
-        dx.zero_()
         L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), "warp bwd")
 
     res = {}

@@ -45,57 +45,75 @@ __device__ __forceinline__ WarpTap warp_tap(int x, int y, float fx, float fy, in
   return t;
 }
 
-__device__ __forceinline__ float warp_sample(const float* __restrict__ im, const WarpTap& t, int w) {
+// one image plane (h*w floats) as a buffer resource: loads at an offset past its end return 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t warp_plane(const float* im, long long hw) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)im, 0, (int)(hw * 4), 0x00020000);
+}
+
+// the four corner values, zero where the corner lies outside the image: an invalid corner
+// gets an out-of-range buffer offset, so the hardware returns 0 and all four loads issue
+// unconditionally, back to back (a zero corner adds +0, exactly as the skipped term would)
+__device__ __forceinline__ void warp_corners(__amdgpu_buffer_rsrc_t im, const WarpTap& t, int w, float& a, float& b,
+                                             float& c, float& d) {
+  constexpr unsigned kOut = 0x80000000u;
+  const unsigned r0 = (unsigned)(t.y0 * w), r1 = (unsigned)((t.y0 + 1) * w);
+  const unsigned oa = (t.vy0 && t.vx0) ? (r0 + t.x0) * 4u : kOut;
+  const unsigned ob = (t.vy0 && t.vx1) ? (r0 + t.x0 + 1) * 4u : kOut;
+  const unsigned oc = (t.vy1 && t.vx0) ? (r1 + t.x0) * 4u : kOut;
+  const unsigned od = (t.vy1 && t.vx1) ? (r1 + t.x0 + 1) * 4u : kOut;
+  a = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(im, oa, 0, 0));
+  b = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(im, ob, 0, 0));
+  c = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(im, oc, 0, 0));
+  d = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(im, od, 0, 0));
+}
+
+__device__ __forceinline__ float warp_sample(__amdgpu_buffer_rsrc_t im, const WarpTap& t, int w) {
+  float a, b, c, d;
+  warp_corners(im, t, w, a, b, c, d);
   float v = 0.f;
-  if (t.vy0 && t.vx0) v += im[(long long)t.y0 * w + t.x0] * t.wnw;
-  if (t.vy0 && t.vx1) v += im[(long long)t.y0 * w + t.x0 + 1] * t.wne;
-  if (t.vy1 && t.vx0) v += im[(long long)(t.y0 + 1) * w + t.x0] * t.wsw;
-  if (t.vy1 && t.vx1) v += im[(long long)(t.y0 + 1) * w + t.x0 + 1] * t.wse;
+  v += a * t.wnw;
+  v += b * t.wne;
+  v += c * t.wsw;
+  v += d * t.wse;
   return v;
 }
 
-__global__ void warp_fwd_kernel(const dvie_warp_desc p) {
+// A wave covers 256 consecutive pixels of one row, 4 per lane 64 apart: each gather
+// instruction then reads the sources of 64 consecutive output pixels (a few cache lines for
+// a smooth flow), and the flow loads and output stores are 256-byte coalesced runs.
+__global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
+  const int segs = (p.w + 255) >> 8;
   const long long hw = (long long)p.h * p.w;
-  const long long total = (long long)p.n * hw;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int x = (int)(e % p.w);
-    const int y = (int)((e / p.w) % p.h);
-    const int n = (int)(e / hw);
-    const long long fo = (long long)y * p.w + x;
-    const WarpTap t = warp_tap(x, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo], p.w,
-                               p.h, p.align_corners);
-    for (int c = 0; c < p.c; ++c) {
-      const long long base = ((long long)n * p.c + c) * hw;
-      p.out[base + fo] = warp_sample(p.img + base, t, p.w);
-    }
-  }
-}
-
-// 4 consecutive pixels per thread (w % 4 == 0): 16-byte flow loads and output stores, 4x
-// the independent gathers in flight per thread; per-pixel arithmetic identical to the above
-__global__ __launch_bounds__(256) void warp_fwd4_kernel(const dvie_warp_desc p) {
-  const int wq = p.w >> 2;
-  const long long hw = (long long)p.h * p.w;
-  const long long total = (long long)p.n * p.h * wq;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int xq = (int)(e % wq);
-    const long long r = e / wq;
-    const int y = (int)(r % p.h), n = (int)(r / p.h);
-    const int x = 4 * xq;
-    const long long fo = (long long)y * p.w + x;
-    const f32x4 fx = *(const f32x4*)(p.flow + (long long)n * 2 * hw + fo);
-    const f32x4 fy = *(const f32x4*)(p.flow + ((long long)n * 2 + 1) * hw + fo);
+  const int waves = p.n * p.h * segs;  // < 2^31 (checked at launch)
+  const int lane = threadIdx.x & 63;
+  // wave-uniform row/segment (readfirstlane), so the plane buffer resources are scalar
+  for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
+       wv += gridDim.x * 4) {
+    const int sg = wv % segs;
+    const int r = wv / segs;
+    const int y = r % p.h, n = r / p.h;
     WarpTap t[4];
+    bool live[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) t[k] = warp_tap(x + k, y, fx[k], fy[k], p.w, p.h, p.align_corners);
+    for (int k = 0; k < 4; ++k) {
+      const int x = (sg << 8) + lane + 64 * k;
+      live[k] = x < p.w;
+      const int xl = live[k] ? x : p.w - 1;  // clamped: the loads stay unconditional
+      const long long fo = (long long)y * p.w + xl;
+      t[k] = warp_tap(xl, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo], p.w, p.h,
+                      p.align_corners);
+    }
     for (int c = 0; c < p.c; ++c) {
-      const long long base = ((long long)n * p.c + c) * hw;
-      f32x4 o;
+      const long long plane = ((long long)n * p.c + c) * hw;
+      const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + plane, hw), out = warp_plane(p.out + plane, hw);
+      float o[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = warp_sample(p.img + base, t[k], p.w);
-      *(f32x4*)(p.out + base + fo) = o;
+      for (int k = 0; k < 4; ++k) o[k] = warp_sample(im, t[k], p.w);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // columns past the row end: out-of-range offset, store dropped
+        const unsigned off = live[k] ? (unsigned)(y * p.w + (sg << 8) + lane + 64 * k) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[k]), out, off, 0, 0);
+      }
     }
   }
 }
@@ -104,33 +122,22 @@ __global__ __launch_bounds__(256) void warp_fwd4_kernel(const dvie_warp_desc p) 
 // d/d(img) of one bilinear corner, and the flow-gradient terms, per channel (order of the
 // reference autograd: corners nw, ne, sw, se)
 template <typename Scatter>
-__device__ __forceinline__ void warp_bwd_pixel(const float* __restrict__ im, float go, const WarpTap& t, int w,
+__device__ __forceinline__ void warp_bwd_pixel(float a, float b, float c, float d, float go, const WarpTap& t,
                                                float& gix, float& giy, Scatter&& scatter) {
   const int x1 = t.x0 + 1, y1 = t.y0 + 1;
-  if (t.vy0 && t.vx0) {
-    const float v = im[(long long)t.y0 * w + t.x0];
-    gix -= v * ((float)y1 - t.iy) * go;
-    giy -= v * ((float)x1 - t.ix) * go;
-    scatter(t.y0, t.x0, t.wnw * go);
-  }
-  if (t.vy0 && t.vx1) {
-    const float v = im[(long long)t.y0 * w + x1];
-    gix += v * ((float)y1 - t.iy) * go;
-    giy -= v * (t.ix - (float)t.x0) * go;
-    scatter(t.y0, x1, t.wne * go);
-  }
-  if (t.vy1 && t.vx0) {
-    const float v = im[(long long)y1 * w + t.x0];
-    gix -= v * (t.iy - (float)t.y0) * go;
-    giy += v * ((float)x1 - t.ix) * go;
-    scatter(y1, t.x0, t.wsw * go);
-  }
-  if (t.vy1 && t.vx1) {
-    const float v = im[(long long)y1 * w + x1];
-    gix += v * (t.iy - (float)t.y0) * go;
-    giy += v * (t.ix - (float)t.x0) * go;
-    scatter(y1, x1, t.wse * go);
-  }
+  // invalid corners contribute exact zeros to the flow terms (their value is 0)
+  gix -= a * ((float)y1 - t.iy) * go;
+  giy -= a * ((float)x1 - t.ix) * go;
+  gix += b * ((float)y1 - t.iy) * go;
+  giy -= b * (t.ix - (float)t.x0) * go;
+  gix -= c * (t.iy - (float)t.y0) * go;
+  giy += c * ((float)x1 - t.ix) * go;
+  gix += d * (t.iy - (float)t.y0) * go;
+  giy += d * (t.ix - (float)t.x0) * go;
+  if (t.vy0 && t.vx0) scatter(t.y0, t.x0, t.wnw * go);
+  if (t.vy0 && t.vx1) scatter(t.y0, x1, t.wne * go);
+  if (t.vy1 && t.vx0) scatter(y1, t.x0, t.wsw * go);
+  if (t.vy1 && t.vx1) scatter(y1, x1, t.wse * go);
 }
 
 __device__ __forceinline__ void warp_store_dflow(const dvie_warp_desc& p, int n, long long fo, float gix, float giy) {
@@ -141,115 +148,136 @@ __device__ __forceinline__ void warp_store_dflow(const dvie_warp_desc& p, int n,
   p.dflow[((long long)n * 2 + 1) * hw + fo] = -giy * sy;
 }
 
-// one global atomic per corner (no workspace)
-__global__ void warp_bwd_kernel(const dvie_warp_desc p) {
+// Image gradient by gathering instead of scattering (LDS float atomics measured at ~100
+// cycles per wave instruction on gfx950, global ones at ~100 G lanes/s: both far below HBM).
+// A dimg pixel c receives the bilinear weight of every sample s (output pixel) that has c as
+// a corner.  Under a smooth flow those samples sit next to s*(c) = c - d(c), d(c) being the
+// integer source displacement (x0 - x, y0 - y) of the sample AT c.  warp_bwd_pull_kernel
+// visits the 4x4 candidates s*(c) + [-2, 1]^2 for every c and STORES dimg (no zero-fill, no
+// atomics, a fixed summation order); warp_bwd_flow_kernel computes dflow and adds, with a
+// global atomic, each (s, c) pair the candidate rule misses (folding / discontinuous flow).
+constexpr int WP_LO = -2, WP_HI = 1;
+
+// s*(c): c minus the integer displacement of the sample at c
+__device__ __forceinline__ int2 warp_pull_origin(const dvie_warp_desc& p, const float* fl0, const float* fl1, int cx,
+                                                 int cy) {
+  const long long fo = (long long)cy * p.w + cx;
+  const WarpTap t = warp_tap(cx, cy, fl0[fo], fl1[fo], p.w, p.h, p.align_corners);
+  return make_int2(2 * cx - t.x0, 2 * cy - t.y0);
+}
+
+// the one ownership rule both passes apply: is sample (sx, sy) a candidate of cell c?
+__device__ __forceinline__ bool warp_pulled(int2 o, int sx, int sy) {
+  return (unsigned)(sx - o.x - WP_LO) <= (unsigned)(WP_HI - WP_LO) &&
+         (unsigned)(sy - o.y - WP_LO) <= (unsigned)(WP_HI - WP_LO);
+}
+
+// a wave covers 256 consecutive dimg pixels of one row (4 per lane, 64 apart)
+__global__ __launch_bounds__(256) void warp_bwd_pull_kernel(const dvie_warp_desc p) {
+  const int segs = (p.w + 255) >> 8;
+  const int waves = p.n * p.h * segs;
+  const int lane = threadIdx.x & 63;
   const long long hw = (long long)p.h * p.w;
-  const long long total = (long long)p.n * hw;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int x = (int)(e % p.w);
-    const int y = (int)((e / p.w) % p.h);
-    const int n = (int)(e / hw);
-    const long long fo = (long long)y * p.w + x;
-    const WarpTap t = warp_tap(x, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo], p.w,
-                               p.h, p.align_corners);
-    float gix = 0.f, giy = 0.f;
-    for (int c = 0; c < p.c; ++c) {
-      const long long base = ((long long)n * p.c + c) * hw;
-      warp_bwd_pixel(p.img + base, p.dout[base + fo], t, p.w, gix, giy, [&](int yy, int xx, float v) {
-        if (p.dimg) atomicAdd(p.dimg + base + (long long)yy * p.w + xx, v);
-      });
+  for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
+       wv += gridDim.x * 4) {
+    const int sg = wv % segs;
+    const int r = wv / segs;
+    const int cy = r % p.h, n = r / p.h;
+    const float* fl0 = p.flow + (long long)n * 2 * hw;
+    const float* fl1 = fl0 + hw;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const int cx = (sg << 8) + lane + 64 * k;
+      if (cx >= p.w) continue;
+      const int2 o = warp_pull_origin(p, fl0, fl1, cx, cy);
+      // phase 1: the 16 candidates' weights for c (0 where c is not one of their corners);
+      // coordinates clamped into the image so the flow loads issue back to back
+      constexpr int NC = (WP_HI - WP_LO + 1) * (WP_HI - WP_LO + 1);
+      float fxs[NC], fys[NC];
+      int fss[NC];
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
+        sx = sx < 0 ? 0 : (sx >= p.w ? p.w - 1 : sx);
+        sy = sy < 0 ? 0 : (sy >= p.h ? p.h - 1 : sy);
+        fss[q] = sy * p.w + sx;
+        fxs[q] = fl0[fss[q]];
+        fys[q] = fl1[fss[q]];
+      }
+      float wq[NC];
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
+        const bool in = (unsigned)sx < (unsigned)p.w && (unsigned)sy < (unsigned)p.h;
+        const WarpTap t = warp_tap(sx, sy, fxs[q], fys[q], p.w, p.h, p.align_corners);
+        const int qx = cx - t.x0, qy = cy - t.y0;  // 0/1: c is the x0/x1, y0/y1 corner of s
+        const float w = qy == 0 ? (qx == 0 ? t.wnw : t.wne) : (qx == 0 ? t.wsw : t.wse);
+        wq[q] = (in && (unsigned)qx <= 1u && (unsigned)qy <= 1u) ? w : 0.f;
+      }
+      // phase 2: dimg[c] = sum over candidates of weight * dout[s], in candidate order
+      // (a zero weight adds +0: the candidate did not hit c)
+      for (int ch = 0; ch < p.c; ++ch) {
+        const float* go = p.dout + ((long long)n * p.c + ch) * hw;
+        float g[NC];
+#pragma unroll
+        for (int q = 0; q < NC; ++q) g[q] = go[fss[q]];
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) acc += wq[q] * g[q];
+        p.dimg[((long long)n * p.c + ch) * hw + (long long)cy * p.w + cx] = acc;
+      }
     }
-    if (p.dflow) warp_store_dflow(p, n, fo, gix, giy);
   }
 }
 
-// tiled image gradient: a workgroup owns WT_H x WT_W output pixels (4 per thread) and
-// accumulates their corner contributions in an LDS copy of its region (the tile grown by
-// WT_M pixels on every side), WT_CB channels at a time; the region is then stored to the
-// workspace and warp_bwd_gather_kernel sums the (at most 4) regions covering each pixel.
-constexpr int WT_W = 64, WT_H = 16, WT_M = 4, WT_CB = 4;
-constexpr int WT_RH = WT_H + 2 * WT_M, WT_RW = WT_W + 2 * WT_M, WT_CELLS = WT_RH * WT_RW;
-
-__global__ __launch_bounds__(256) void warp_bwd_tile_kernel(const dvie_warp_desc p, int tiles_x, int tiles_y) {
-  __shared__ float acc[WT_CB * WT_CELLS];
-  const int tx = blockIdx.x % tiles_x;
-  const int ty = (blockIdx.x / tiles_x) % tiles_y;
-  const int n = blockIdx.x / (tiles_x * tiles_y);
-  const int x = tx * WT_W + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
-  const int oy = ty * WT_H - WT_M, ox = tx * WT_W - WT_M;  // region origin
+// dflow for every sample and, with dimg, the (sample, corner) pairs the pull pass misses
+// (global atomics, launched after it).  A wave covers 256 consecutive pixels of a row (4 per
+// lane, 64 apart), so the image planes are wave-uniform buffer resources.
+__global__ __launch_bounds__(256) void warp_bwd_flow_kernel(const dvie_warp_desc p) {
+  const int segs = (p.w + 255) >> 8;
+  const int waves = p.n * p.h * segs;
+  const int lane = threadIdx.x & 63;
   const long long hw = (long long)p.h * p.w;
-  WarpTap t[WT_H / 4];
-  bool live[WT_H / 4];
-  float gix[WT_H / 4], giy[WT_H / 4];
+  for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
+       wv += gridDim.x * 4) {
+    const int sg = wv % segs;
+    const int r = wv / segs;
+    const int y = r % p.h, n = r / p.h;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const int x = (sg << 8) + lane + 64 * k;
+      const bool live = x < p.w;
+      const int xl = live ? x : p.w - 1;
+      const long long fo = (long long)y * p.w + xl;
+      const WarpTap t = warp_tap(xl, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo],
+                                 p.w, p.h, p.align_corners);
+      // (sample, corner) pairs the pull pass misses (evaluated once, shared by all channels)
+      bool far[4] = {false, false, false, false};
+      if (p.dimg && live) {
+        const float* fl0 = p.flow + (long long)n * 2 * hw;
+        const int cxs[4] = {t.x0, t.x0 + 1, t.x0, t.x0 + 1}, cys[4] = {t.y0, t.y0, t.y0 + 1, t.y0 + 1};
+        const bool val[4] = {t.vy0 && t.vx0, t.vy0 && t.vx1, t.vy1 && t.vx0, t.vy1 && t.vx1};
 #pragma unroll
-  for (int k = 0; k < WT_H / 4; ++k) {
-    const int y = ty * WT_H + rg + 4 * k;
-    live[k] = x < p.w && y < p.h;
-    gix[k] = giy[k] = 0.f;
-    if (live[k]) {
-      const long long fo = (long long)y * p.w + x;
-      t[k] = warp_tap(x, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo], p.w, p.h,
-                      p.align_corners);
-    }
-  }
-  float* region = p.ws + (((long long)n * tiles_y + ty) * tiles_x + tx) * (long long)p.c * WT_CELLS;
-  for (int c0 = 0; c0 < p.c; c0 += WT_CB) {
-    const int cb = p.c - c0 < WT_CB ? p.c - c0 : WT_CB;
-    for (int i = threadIdx.x; i < cb * WT_CELLS; i += 256) acc[i] = 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < WT_H / 4; ++k) {
-      if (!live[k]) continue;
-      const long long fo = (long long)(ty * WT_H + rg + 4 * k) * p.w + x;
-      for (int cc = 0; cc < cb; ++cc) {
-        const long long base = ((long long)n * p.c + c0 + cc) * hw;
-        float* lds = acc + cc * WT_CELLS;
-        warp_bwd_pixel(p.img + base, p.dout[base + fo], t[k], p.w, gix[k], giy[k], [&](int yy, int xx, float v) {
-          const int ly = yy - oy, lx = xx - ox;
-          if ((unsigned)ly < (unsigned)WT_RH && (unsigned)lx < (unsigned)WT_RW)
-            atomicAdd(lds + ly * WT_RW + lx, v);
-          else
-            atomicAdd(p.dimg + base + (long long)yy * p.w + xx, v);  // far sample: rare
-        });
+        for (int q = 0; q < 4; ++q)
+          if (val[q]) far[q] = !warp_pulled(warp_pull_origin(p, fl0, fl0 + hw, cxs[q], cys[q]), xl, y);
       }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < cb * WT_CELLS; i += 256) region[(long long)c0 * WT_CELLS + i] = acc[i];
-    __syncthreads();
-  }
-  if (p.dflow) {
-#pragma unroll
-    for (int k = 0; k < WT_H / 4; ++k)
-      if (live[k]) warp_store_dflow(p, n, (long long)(ty * WT_H + rg + 4 * k) * p.w + x, gix[k], giy[k]);
-  }
-}
-
-__device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
-
-__global__ __launch_bounds__(256) void warp_bwd_gather_kernel(const dvie_warp_desc p, int tiles_x, int tiles_y) {
-  const long long hw = (long long)p.h * p.w;
-  const long long total = (long long)p.n * p.c * hw;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int x = (int)(e % p.w);
-    const int y = (int)((e / p.w) % p.h);
-    const long long nc = e / hw;
-    const int c = (int)(nc % p.c), n = (int)(nc / p.c);
-    int ty0 = floordiv(y - WT_M, WT_H), ty1 = (y + WT_M) / WT_H;
-    int tx0 = floordiv(x - WT_M, WT_W), tx1 = (x + WT_M) / WT_W;
-    ty0 = ty0 < 0 ? 0 : ty0;
-    tx0 = tx0 < 0 ? 0 : tx0;
-    ty1 = ty1 > tiles_y - 1 ? tiles_y - 1 : ty1;
-    tx1 = tx1 > tiles_x - 1 ? tiles_x - 1 : tx1;
-    float s = p.dimg[e];  // far samples (global atomics of the tile pass)
-    for (int ty = ty0; ty <= ty1; ++ty)
-      for (int tx = tx0; tx <= tx1; ++tx) {
-        const int ly = y - (ty * WT_H - WT_M), lx = x - (tx * WT_W - WT_M);
-        s += p.ws[((((long long)n * tiles_y + ty) * tiles_x + tx) * p.c + c) * WT_CELLS + ly * WT_RW + lx];
+      const bool any_far = far[0] || far[1] || far[2] || far[3];
+      float gix = 0.f, giy = 0.f;
+      for (int c = 0; c < p.c; ++c) {
+        const long long base = ((long long)n * p.c + c) * hw;
+        float a, b, cc, dd;
+        warp_corners(warp_plane(p.img + base, hw), t, p.w, a, b, cc, dd);
+        const float go = p.dout[base + fo];
+        warp_bwd_pixel(a, b, cc, dd, go, t, gix, giy, [](int, int, float) {});
+        if (any_far) {
+          if (far[0]) atomicAdd(p.dimg + base + (long long)t.y0 * p.w + t.x0, t.wnw * go);
+          if (far[1]) atomicAdd(p.dimg + base + (long long)t.y0 * p.w + t.x0 + 1, t.wne * go);
+          if (far[2]) atomicAdd(p.dimg + base + (long long)(t.y0 + 1) * p.w + t.x0, t.wsw * go);
+          if (far[3]) atomicAdd(p.dimg + base + (long long)(t.y0 + 1) * p.w + t.x0 + 1, t.wse * go);
+        }
       }
-    p.dimg[e] = s;
+      if (p.dflow && live) warp_store_dflow(p, n, fo, gix, giy);
+    }
   }
 }
 
@@ -291,42 +319,26 @@ extern "C" {
 
 int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->out && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
-  const bool v4 = d->w % 4 == 0 && (((uintptr_t)d->flow | (uintptr_t)d->out) & 15) == 0;
-  if (v4)
-    hipLaunchKernelGGL(warp_fwd4_kernel, dim3(grid_for((long long)d->n * d->h * (d->w / 4))), dim3(256), 0,
-                       (hipStream_t)stream, *d);
-  else
-    hipLaunchKernelGGL(warp_fwd_kernel, dim3(grid_for((long long)d->n * d->h * d->w)), dim3(256), 0,
-                       (hipStream_t)stream, *d);
+  const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
+  DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
+  hipLaunchKernelGGL(warp_fwd_kernel, dim3(grid_for(waves * 256)), dim3(256), 0, (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
 
-static void warp_tiles(const dvie_warp_desc* d, int& tx, int& ty) {
-  tx = (d->w + WT_W - 1) / WT_W;
-  ty = (d->h + WT_H - 1) / WT_H;
-}
 
 size_t dvie_warp_ws_floats(const dvie_warp_desc* d) {
-  if (!d || d->n <= 0 || d->c <= 0 || d->h <= 0 || d->w <= 0) return 0;
-  int tx, ty;
-  warp_tiles(d, tx, ty);
-  return (size_t)d->n * ty * tx * d->c * WT_CELLS;
+  (void)d;
+  return 0;  // the backward needs no workspace (kept for ABI stability)
 }
 
 int dvie_warp_bwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->dout && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
+  DVIE_CHECK_ARG((long long)d->h * d->w < (1LL << 29), "warp: size");
   hipStream_t s = (hipStream_t)stream;
-  if (d->ws && d->dimg) {
-    int tx, ty;
-    warp_tiles(d, tx, ty);
-    const long long blocks = (long long)d->n * ty * tx;
-    DVIE_CHECK_ARG(blocks < (1LL << 31), "warp: grid");
-    hipLaunchKernelGGL(warp_bwd_tile_kernel, dim3((unsigned)blocks), dim3(256), 0, s, *d, tx, ty);
-    hipLaunchKernelGGL(warp_bwd_gather_kernel, dim3(grid_for((long long)d->n * d->c * d->h * d->w)), dim3(256), 0, s,
-                       *d, tx, ty);
-  } else {
-    hipLaunchKernelGGL(warp_bwd_kernel, dim3(grid_for((long long)d->n * d->h * d->w)), dim3(256), 0, s, *d);
-  }
+  const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
+  DVIE_CHECK_ARG(waves < (1LL << 31), "warp: size");
+  if (d->dimg) hipLaunchKernelGGL(warp_bwd_pull_kernel, dim3(grid_for(waves * 256)), dim3(256), 0, s, *d);
+  hipLaunchKernelGGL(warp_bwd_flow_kernel, dim3(grid_for(waves * 256)), dim3(256), 0, s, *d);
   DVIE_RETURN_LAUNCH();
 }
 

@@ -34,7 +34,7 @@ class _WarpFn(torch.autograd.Function):
     def backward(ctx, go):
         x, flow = ctx.saved_tensors
         go = go.float().contiguous()
-        dx = torch.zeros_like(x) if ctx.needs_input_grad[0] else None
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None  # overwritten
         dflow = torch.empty_like(flow) if ctx.needs_input_grad[1] else None
         n, c, h, w = x.shape
         d = L.WarpDesc()
@@ -42,11 +42,6 @@ class _WarpFn(torch.autograd.Function):
         d.dimg = dx.data_ptr() if dx is not None else None
         d.dflow = dflow.data_ptr() if dflow is not None else None
         d.n, d.c, d.h, d.w, d.align_corners = n, c, h, w, int(ctx.ac)
-        ws = None
-        if dx is not None:  # tiled image gradient: per-tile LDS aggregation + gather pass
-            ws = torch.empty(max(1, L.load().dvie_warp_ws_floats(ctypes.byref(d))), dtype=torch.float32,
-                             device=x.device)
-            d.ws = ws.data_ptr()
         L.check(L.load().dvie_warp_bwd(ctypes.byref(d), L.stream_ptr(x.device)), "warp bwd")
         return dx, dflow, None
 

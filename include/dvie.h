@@ -265,11 +265,11 @@ size_t dvie_loss_ws_floats(const dvie_loss_desc* d);
  * zeros padding, align_corners=True as in the pinned torch 1.0.1):
  *   gx = linspace(-1,1,W)[x] - flow[n,0,y,x],  gy = linspace(-1,1,H)[y] - flow[n,1,y,x]
  *   out[n,c,y,x] = bilinear(img[n,c], (gx+1)/2*(W-1), (gy+1)/2*(H-1))
- * fp32, NCHW contiguous.  Backward: dimg (accumulated — zero it first) and dflow
- * (overwritten), given dout.  With a workspace `ws` of dvie_warp_ws_floats(d) floats the
- * image gradient is aggregated per tile in LDS and written through per-tile partial regions
- * summed by a second gather pass (only samples that land outside their tile's region use
- * global atomics); ws = NULL: one global atomic per bilinear corner.
+ * fp32, NCHW contiguous.  Backward: dimg and dflow (both overwritten), given dout.  dimg
+ * is produced by ownership: one workgroup per 64x16 tile of dimg sums, in LDS, the corners
+ * of the samples in its flow-displaced window and stores the tile; a second pass computes
+ * dflow and adds the few corners no window owns (large or discontinuous flow) with global
+ * atomics.  dimg = NULL computes dflow only.  `ws` is reserved (dvie_warp_ws_floats = 0).
  */
 typedef struct dvie_warp_desc {
   const float* img;
