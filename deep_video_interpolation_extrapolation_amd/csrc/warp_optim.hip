@@ -185,46 +185,51 @@ __global__ __launch_bounds__(256) void warp_bwd_pull_kernel(const dvie_warp_desc
     const int cy = r % p.h, n = r / p.h;
     const float* fl0 = p.flow + (long long)n * 2 * hw;
     const float* fl1 = fl0 + hw;
+    const __amdgpu_buffer_rsrc_t rf0 = warp_plane(fl0, hw), rf1 = warp_plane(fl1, hw);
 #pragma unroll 1
     for (int k = 0; k < 4; ++k) {
       const int cx = (sg << 8) + lane + 64 * k;
       if (cx >= p.w) continue;
       const int2 o = warp_pull_origin(p, fl0, fl1, cx, cy);
-      // phase 1: the 16 candidates' weights for c (0 where c is not one of their corners);
-      // coordinates clamped into the image so the flow loads issue back to back
+      // phase 1: the 16 candidates' weights for c (0 where c is not one of their corners).
+      // Buffer loads with 32-bit offsets; a candidate outside the image gets an out-of-range
+      // offset (loads return 0) and a zero weight, so every load issues unconditionally.
       constexpr int NC = (WP_HI - WP_LO + 1) * (WP_HI - WP_LO + 1);
+      unsigned off[NC];
       float fxs[NC], fys[NC];
-      int fss[NC];
 #pragma unroll
       for (int q = 0; q < NC; ++q) {
-        int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
-        sx = sx < 0 ? 0 : (sx >= p.w ? p.w - 1 : sx);
-        sy = sy < 0 ? 0 : (sy >= p.h ? p.h - 1 : sy);
-        fss[q] = sy * p.w + sx;
-        fxs[q] = fl0[fss[q]];
-        fys[q] = fl1[fss[q]];
+        const int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
+        const bool in = (unsigned)sx < (unsigned)p.w && (unsigned)sy < (unsigned)p.h;
+        off[q] = in ? (unsigned)(sy * p.w + sx) * 4u : 0x80000000u;
+        fxs[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf0, off[q], 0, 0));
+        fys[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf1, off[q], 0, 0));
       }
       float wq[NC];
 #pragma unroll
       for (int q = 0; q < NC; ++q) {
         const int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
-        const bool in = (unsigned)sx < (unsigned)p.w && (unsigned)sy < (unsigned)p.h;
-        const WarpTap t = warp_tap(sx, sy, fxs[q], fys[q], p.w, p.h, p.align_corners);
-        const int qx = cx - t.x0, qy = cy - t.y0;  // 0/1: c is the x0/x1, y0/y1 corner of s
-        const float w = qy == 0 ? (qx == 0 ? t.wnw : t.wne) : (qx == 0 ? t.wsw : t.wse);
-        wq[q] = (in && (unsigned)qx <= 1u && (unsigned)qy <= 1u) ? w : 0.f;
+        const float ix = unnorm(linspace_pm1(sx, p.w) - fxs[q], p.w, p.align_corners);
+        const float iy = unnorm(linspace_pm1(sy, p.h) - fys[q], p.h, p.align_corners);
+        const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+        const int qx = cx - x0, qy = cy - y0;  // 0/1: c is the x0/x1, y0/y1 corner of s
+        // the bilinear weight exactly as warp_tap forms it (wnw / wne / wsw / wse)
+        const float w = (qx == 0 ? (float)(x0 + 1) - ix : ix - (float)x0) *
+                        (qy == 0 ? (float)(y0 + 1) - iy : iy - (float)y0);
+        wq[q] = (off[q] != 0x80000000u && (unsigned)qx <= 1u && (unsigned)qy <= 1u) ? w : 0.f;
       }
       // phase 2: dimg[c] = sum over candidates of weight * dout[s], in candidate order
       // (a zero weight adds +0: the candidate did not hit c)
       for (int ch = 0; ch < p.c; ++ch) {
-        const float* go = p.dout + ((long long)n * p.c + ch) * hw;
+        const long long plane = ((long long)n * p.c + ch) * hw;
+        const __amdgpu_buffer_rsrc_t rg = warp_plane(p.dout + plane, hw);
         float g[NC];
 #pragma unroll
-        for (int q = 0; q < NC; ++q) g[q] = go[fss[q]];
+        for (int q = 0; q < NC; ++q) g[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, off[q], 0, 0));
         float acc = 0.f;
 #pragma unroll
         for (int q = 0; q < NC; ++q) acc += wq[q] * g[q];
-        p.dimg[((long long)n * p.c + ch) * hw + (long long)cy * p.w + cx] = acc;
+        p.dimg[plane + (long long)cy * p.w + cx] = acc;
       }
     }
   }
