@@ -124,6 +124,37 @@ def warp_roofline(dev, n, H, W, reps=20):
     return res
 
 
+def clip_prep_roofline(dev, n, H, W, reps=20):
+    """Device clip pipeline (data.DeviceClips / dvie_clip_prep; the reference's DataLoader
+    worker, folder.py:207-247): n 3-frame clips from an HBM-resident uint8 store of
+    (H+22)x(W+22) frames, flipped + pseudo-motion cropped to HxW, normalised, 20-class
+    one-hot.  Algorithmic bytes per output pixel: read RGB 3 + label 1, write 12 + 80 = 96."""
+    import random
+    import numpy as np
+    from deep_video_interpolation_extrapolation_amd.data import DeviceClips
+    g = torch.Generator(device=dev).manual_seed(3)
+    h0, w0 = H + 22, W + 22
+    imgs = torch.randint(0, 256, (n, 3, h0, w0, 3), generator=g, device=dev, dtype=torch.uint8)
+    segs = torch.randint(0, 20, (n, 3, h0, w0), generator=g, device=dev, dtype=torch.uint8)
+    dc = DeviceClips(imgs, segs, crop=(H, W), device=dev, strict=False)
+    params = dc.draw_params(n, np.random.RandomState(0), random.Random(0))
+    idx = list(range(n))
+    for _ in range(3):
+        dc.batch(idx, params)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        dc.batch(idx, params)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    gbs = 100.0 * n * 3 * H * W / (ms * 1e-3) / 1e9
+    return {"clips": n, "frames": 3 * n, "shape": [H, W], "ms": round(ms, 4), "GBps": round(gbs, 1),
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_px": 100,
+            "note": "per batch call incl. its small host->device index/param copies and output allocation"}
+
+
 def main():
     a = parse()
     os.environ["DVIE_PRECISION"] = a.precision
@@ -249,6 +280,7 @@ def main():
         }
         out["warp"] = warp_roofline(dev, a.batch, a.height, a.width)
         out["warp_1024x2048"] = warp_roofline(dev, a.batch, 1024, 2048, reps=5)  # BASELINE configs[4] frames
+        out["clip_prep"] = clip_prep_roofline(dev, a.batch, a.height, a.width)
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.height, a.width)
         else:

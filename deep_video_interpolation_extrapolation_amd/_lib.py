@@ -114,6 +114,14 @@ class WarpDesc(ctypes.Structure):
     ]
 
 
+class ClipDesc(ctypes.Structure):
+    _fields_ = [
+        ("img", vp), ("seg", vp), ("idx", vp), ("params", vp), ("frames", vp), ("segs", vp), ("bad", vp),
+        ("b", i32), ("t", i32), ("h0", i32), ("w0", i32), ("hc", i32), ("wc", i32),
+        ("n_classes", i32), ("pad0", i32),
+    ]
+
+
 class BnDesc(ctypes.Structure):
     _fields_ = [
         ("x", vp), ("y", vp), ("g", vp), ("dx", vp), ("gamma", vp), ("beta", vp), ("dgamma", vp), ("dbeta", vp),
@@ -168,7 +176,7 @@ class Op(ctypes.Structure):
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
-        100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer}
+        100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
 
 EXPORTS = [
     "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
@@ -176,7 +184,7 @@ EXPORTS = [
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
-    "dvie_reparam_bwd", "dvie_warp_ws_floats",
+    "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep",
 ]
 
 _lib = None
@@ -210,7 +218,7 @@ def load():
         lib.dvie_last_error.restype = ctypes.c_char_p
         for name in ("dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_ew",
                      "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_head_fwd",
-                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd"):
+                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_clip_prep"):
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]

@@ -409,6 +409,7 @@ size_t dvie_abi_sizeof(int which) {
     case 100: return sizeof(dvie_warp_desc);
     case 101: return sizeof(dvie_softmax_desc);
     case 102: return sizeof(dvie_sn_layer);
+    case 103: return sizeof(dvie_clip_desc);
     default: return 0;
   }
 }

@@ -19,6 +19,7 @@
 #define DVIE_H
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -463,6 +464,34 @@ typedef struct dvie_op {
     dvie_head_desc head;
   } u;
 } dvie_op;
+
+/*
+ * Cityscapes clip preparation on the device (reference folder.py:225-247 train branch and
+ * l.248-261 val branch; crop parameters folder.py:125-149, flip l.211).  Replaces the
+ * DataLoader worker's PIL flip / crop, to_tensor, normalize((.5,.5,.5),(.5,.5,.5)) and
+ * np.eye(20)[seg] one-hot.  For clip b (dataset clip idx[b]) and frame t with
+ * params[(b*T+t)*3 + {0,1,2}] = {flip, h1, w1}:
+ *   src_x = flip ? W0-1-(w1+x) : w1+x,  src_y = h1+y      (flip the full frame, then crop)
+ *   frames[t][b][c][y][x] = (img[idx[b]][t][src_y][src_x][c] / 255 - 0.5) / 0.5   (fp32)
+ *   segs[t][b][k][y][x]   = (seg[idx[b]][t][src_y][src_x] == k)                      (fp32)
+ * img: uint8 (N, T, H0, W0, 3) RGB as decoded, seg: uint8 (N, T, H0, W0) class ids (NULL:
+ * no segs), both HBM-resident.  A label >= n_classes (np.eye raises IndexError there)
+ * gives an all-zero one-hot and is counted into *bad (optional, accumulated).  idx = NULL
+ * means clip b = b.  Every read must stay inside the frame: h1 + hc <= h0, w1 + wc <= w0
+ * (the caller's crop generator guarantees it; not re-checked per pixel).
+ */
+typedef struct dvie_clip_desc {
+  const uint8_t* img;
+  const uint8_t* seg;
+  const int* idx;
+  const int* params;
+  float* frames;
+  float* segs;
+  int* bad;
+  int b, t, h0, w0, hc, wc, n_classes, pad0;
+} dvie_clip_desc;
+
+int dvie_clip_prep(const dvie_clip_desc* d, void* stream);
 
 int dvie_run_ops(const dvie_op* ops, int n, void* stream);
 

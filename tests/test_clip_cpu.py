@@ -1,0 +1,43 @@
+"""Device clip pipeline, host side (no GPU): the product's pseudo-motion crop generator
+against the oracle's restatement of folder.py:125-149 (same np.random stream, exact), the
+oracle's flip / crop / normalise / one-hot against direct numpy indexing, and the loud
+failure off-GPU."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import clip as OC
+
+
+def test_crop_params_match_oracle():
+    from deep_video_interpolation_extrapolation_amd.data import seq_crop_params
+    for seed in range(50):
+        a = seq_crop_params(150, 150, 128, 128, np.random.RandomState(seed))
+        b = OC.seq_crop_params(150, 150, 128, 128, np.random.RandomState(seed))
+        assert a == b
+        for h1, w1, h, w in a:
+            assert 0 <= h1 and h1 + h <= 150 and 0 <= w1 and w1 + w <= 150
+
+
+def test_oracle_matches_indexing():
+    rs = np.random.RandomState(3)
+    imgs = [rs.randint(0, 256, (40, 52, 3), dtype=np.uint8) for _ in range(3)]
+    segs = [rs.randint(0, 20, (40, 52), dtype=np.uint8) for _ in range(3)]
+    crops = OC.seq_crop_params(40, 52, 32, 44, rs)
+    for flip in (0, 1):
+        fr, oh = OC.prep_clip(imgs, segs, flip, crops)
+        for i, (h1, w1, h, w) in enumerate(crops):
+            src = imgs[i][:, ::-1] if flip else imgs[i]
+            ref = src[h1:h1 + h, w1:w1 + w].astype(np.float32)
+            exp = (torch.from_numpy(ref).permute(2, 0, 1) / 255 - 0.5) / 0.5
+            assert torch.equal(fr[i], exp)
+            lab = (segs[i][:, ::-1] if flip else segs[i])[h1:h1 + h, w1:w1 + w]
+            assert torch.equal(oh[i].argmax(0), torch.from_numpy(lab.astype(np.int64)))
+            assert torch.equal(oh[i].sum(0), torch.ones(h, w))
+
+
+def test_device_clips_refuses_cpu():
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    from deep_video_interpolation_extrapolation_amd.data import DeviceClips
+    with pytest.raises(L.DvieError):
+        DeviceClips(torch.zeros((2, 3, 20, 20, 3), dtype=torch.uint8), crop=(16, 16))
