@@ -157,3 +157,40 @@ class DeviceClips:
         mine = perm[rank::world][:per]
         for s in range(0, len(mine) - (batch_size - 1 if drop_last else 0), batch_size):
             yield self.batch(mine[s:s + batch_size])
+
+
+def load_clip_store(path, split, crop, device):
+    """DeviceClips from a decoded uint8 store (npz, loaded without pickle).  Keys: imgs
+    (N, 3, H0, W0, 3) and optional segs (N, 3, H0, W0) for training; val_imgs / val_segs
+    for validation (fall back to imgs / segs).  The store is copied to HBM once."""
+    with np.load(path, allow_pickle=False) as z:
+        pre = "val_" if split != "train" and "val_imgs" in z.files else ""
+        imgs = torch.from_numpy(np.ascontiguousarray(z[pre + "imgs"]))
+        segs = torch.from_numpy(np.ascontiguousarray(z[pre + "segs"])) if pre + "segs" in z.files else None
+    return DeviceClips(imgs, segs, crop=crop if split == "train" else None,
+                       split="train" if split == "train" else "val", device=device)
+
+
+class DeviceClipLoader:
+    """DataLoader stand-in over `DeviceClips` (the reference's DataLoader + DistributedSampler
+    pair, InterTrainer.py:86-96): each rank iterates its rank-strided shard of a permutation
+    seeded by the epoch (`set_epoch`, as DistributedSampler.set_epoch), one prepared batch of
+    `batch_size` clips per step, already on the device.  The last partial batch is dropped
+    (every rank runs the same number of steps, so the gradient all-reduce stays matched)."""
+
+    def __init__(self, clips, batch_size, rank=0, world=1, shuffle=True, seed=0):
+        self.clips, self.bs, self.rank, self.world = clips, max(1, batch_size), rank, world
+        self.shuffle, self.seed, self.ep = shuffle, seed, 0
+        self.sampler = self
+
+    def set_epoch(self, epoch):
+        self.ep = epoch
+
+    def __len__(self):
+        return (len(self.clips) // self.world) // self.bs
+
+    def __iter__(self):
+        if self.shuffle:
+            return self.clips.epoch(self.bs, self.rank, self.world, seed=self.seed + self.ep)
+        mine = np.arange(len(self.clips))[self.rank::self.world][:len(self.clips) // self.world]
+        return (self.clips.batch(mine[s:s + self.bs]) for s in range(0, len(self) * self.bs, self.bs))

@@ -31,11 +31,13 @@ def get_exp_path(args):
 def get_logger(path, rank=0):
     logger = logging.getLogger(f"dvie.rank{rank}")
     logger.setLevel(logging.INFO if rank == 0 else logging.WARNING)
-    if not logger.handlers:
-        fmt = logging.Formatter("%(asctime)s %(message)s")
-        for h in (logging.StreamHandler(), logging.FileHandler(path)):
-            h.setFormatter(fmt)
-            logger.addHandler(h)
+    for h in list(logger.handlers):  # a second main() in one process logs to its own file
+        logger.removeHandler(h)
+        h.close()
+    fmt = logging.Formatter("%(asctime)s %(message)s")
+    for h in (logging.StreamHandler(), logging.FileHandler(path)):
+        h.setFormatter(fmt)
+        logger.addHandler(h)
     return logger
 
 

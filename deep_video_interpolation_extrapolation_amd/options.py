@@ -4,6 +4,10 @@ Same flags / dests / defaults for the global options and the EXTRA and INTER sub
 (so reference command lines parse unchanged), plus MI355X-path additions:
   --precision {fp32,bf16}   compute dtype of the HIP plan (fp32 = parity mode)
   --synthetic N             use N synthetic Cityscapes-shaped clips (no dataset on disk)
+  --clip_store F.npz        decoded uint8 clip store (imgs (N,3,H0,W0,3), segs (N,3,H0,W0),
+                            optional val_imgs / val_segs) kept in HBM and prepared on the GPU
+                            by data.DeviceClips (train: flip + pseudo-motion crop to input_h x
+                            input_w; val: whole frames)
 """
 import argparse
 
@@ -56,6 +60,7 @@ GLOBAL = [
     # MI355X-path additions
     ("--precision", "precision", str, "fp32", ["fp32", "bf16"]),
     ("--synthetic", "synthetic", int, 0, None),
+    ("--clip_store", "clip_store", str, None, None),
 ]
 
 EXTRA = [

@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from .. import nets
-from ..data import batch_to, get_dataset
+from ..data import DeviceClipLoader, batch_to, get_dataset, load_clip_store
 from ..losses import IoU, L1Loss, PSNR, RGBLoss, SegCrossEntropy, SSIM, VGGCosineLoss
 from ..optim import Adamax
 from ..utils.net_utils import AverageMeter
@@ -69,19 +69,32 @@ class InterTrainer:
             self.RGBLoss = RGBLoss(args).to(self.device)
             self.SegLoss = SegCrossEntropy()
             self.coarse_opt = Adamax(list(self.model.module.coarse_model.parameters()), lr=args.coarse_learning_rate)
-            sampler = torch.utils.data.distributed.DistributedSampler(self.train_set) if self.W > 1 else None
-            self.train_loader = torch.utils.data.DataLoader(
-                self.train_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
-                num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
+            if getattr(args, "clip_store", None):
+                self.train_loader = self._device_loader("train", shuffle=True)
+            else:
+                sampler = torch.utils.data.distributed.DistributedSampler(self.train_set) if self.W > 1 else None
+                self.train_loader = torch.utils.data.DataLoader(
+                    self.train_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
+                    num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
         elif args.split == "val":
             self.L1Loss, self.PSNRLoss, self.SSIMLoss = L1Loss(), PSNR(), SSIM()
             self.IoULoss, self.VGGCosLoss = IoU(), VGGCosineLoss().to(self.device)
-            sampler = torch.utils.data.distributed.DistributedSampler(self.val_set) if self.W > 1 else None
-            self.val_loader = torch.utils.data.DataLoader(
-                self.val_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
-                num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
+            if getattr(args, "clip_store", None):
+                self.val_loader = self._device_loader("val", shuffle=False)
+            else:
+                sampler = torch.utils.data.distributed.DistributedSampler(self.val_set) if self.W > 1 else None
+                self.val_loader = torch.utils.data.DataLoader(
+                    self.val_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
+                    num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
         if getattr(args, "resume", False) or getattr(args, "load_coarse", False):
             self.load_checkpoint()
+
+    def _device_loader(self, split, shuffle):
+        """--clip_store: the decoded clips stay in HBM and each batch is prepared by one HIP
+        launch (data.DeviceClips) instead of CPU DataLoader workers."""
+        clips = load_clip_store(self.args.clip_store, split, (self.args.input_h, self.args.input_w), self.device)
+        return DeviceClipLoader(clips, self.args.batch_size // self.args.gpus, self.rank, self.W,
+                                shuffle=shuffle, seed=getattr(self.args, "seed", 0))
 
     # ---------------- the hot path ----------------
     def get_input(self, data):
@@ -118,8 +131,9 @@ class InterTrainer:
     def set_epoch(self, epoch):
         self.log.info("Start of epoch %d" % (epoch + 1))
         self.epoch = epoch + 1
-        if isinstance(getattr(self.train_loader, "sampler", None), torch.utils.data.distributed.DistributedSampler):
-            self.train_loader.sampler.set_epoch(epoch)
+        sampler = getattr(self.train_loader, "sampler", None)
+        if isinstance(sampler, (torch.utils.data.distributed.DistributedSampler, DeviceClipLoader)):
+            sampler.set_epoch(epoch)
 
     def train(self):
         if self.rank == 0:

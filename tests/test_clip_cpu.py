@@ -41,3 +41,16 @@ def test_device_clips_refuses_cpu():
     from deep_video_interpolation_extrapolation_amd.data import DeviceClips
     with pytest.raises(L.DvieError):
         DeviceClips(torch.zeros((2, 3, 20, 20, 3), dtype=torch.uint8), crop=(16, 16))
+
+
+def test_clip_store_option_and_no_cpu_fallback(tmp_path):
+    """--clip_store parses, and a store refuses a CPU device (no CPU fallback)."""
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    from deep_video_interpolation_extrapolation_amd.data import load_clip_store
+    from deep_video_interpolation_extrapolation_amd.options import Options
+    args = Options().parse(["--clip_store", "c.npz", "INTER"])
+    assert args.clip_store == "c.npz"
+    store = tmp_path / "c.npz"
+    np.savez(store, imgs=np.zeros((2, 3, 8, 8, 3), np.uint8), segs=np.zeros((2, 3, 8, 8), np.uint8))
+    with pytest.raises(L.DvieError):
+        load_clip_store(str(store), "train", (4, 4), torch.device("cpu"))

@@ -66,3 +66,47 @@ def test_frames_only_and_epoch(dev):
     batches = list(dc.epoch(2, rank=1, world=2, seed=3))
     assert len(batches) == 1 and batches[0]["frame1"].shape == (2, 3, 32, 40)
     assert float(batches[0]["frame2"].abs().max()) <= 1.0
+
+
+def test_device_loader_shards_and_epochs(dev):
+    """DeviceClipLoader: rank shards of one epoch partition the store, set_epoch reshuffles,
+    and the unshuffled (val) order is the rank-strided identity."""
+    from deep_video_interpolation_extrapolation_amd.data import DeviceClipLoader, DeviceClips
+    imgs, segs = _store(8, 3, 20, 36, 5)
+    dc = DeviceClips(torch.from_numpy(imgs), torch.from_numpy(segs), split="val", device=dev)
+    key = lambda f: int(((f[0, 0, 0] * .5 + .5) * 255).round())  # first byte of a clip's frame 1
+    firsts = {int(imgs[k, 0, 0, 0, 0]): k for k in range(8)}
+    assert len(firsts) == 8
+    seen = []
+    for r in range(2):
+        ld = DeviceClipLoader(dc, 2, rank=r, world=2, shuffle=True, seed=3)
+        assert len(ld) == 2
+        for b in ld:
+            seen += [firsts[key(b["frame1"][i])] for i in range(b["frame1"].shape[0])]
+    assert sorted(seen) == list(range(8))
+    ld = DeviceClipLoader(dc, 2, rank=0, world=2, shuffle=True, seed=3)
+    for ep in (0, 1):
+        ld.set_epoch(ep)
+        got = [firsts[key(b["frame1"][i])] for b in ld for i in range(2)]
+        assert got == list(np.random.RandomState(3 + ep).permutation(8)[0::2])
+    ld = DeviceClipLoader(dc, 2, rank=1, world=2, shuffle=False)
+    assert [firsts[key(b["frame1"][i])] for b in ld for i in range(2)] == [1, 3, 5, 7]
+
+
+def test_main_launcher_clip_store(dev, tmp_path):
+    """The launcher with --clip_store: one epoch of training on HBM-resident uint8 clips
+    cropped on the GPU, the checkpoint, and validation on whole frames from the store."""
+    from deep_video_interpolation_extrapolation_amd import main as M
+    imgs, segs = _store(4, 3, 40, 72, 9)
+    vimgs, vsegs = _store(2, 3, 32, 64, 10)
+    store = tmp_path / "clips.npz"
+    np.savez(store, imgs=imgs, segs=segs, val_imgs=vimgs, val_segs=vsegs)
+    common = ["--syn_type", "inter", "--bs", "2", "--input_h", "32", "--input_w", "64", "--epochs", "1",
+              "--save_dir", str(tmp_path / "log"), "--clip_store", str(store), "--nw", "0", "--precision", "fp32"]
+    M.main(common + ["INTER", "--train_coarse"])
+    run = next((tmp_path / "log").iterdir())
+    ck = next((run / "checkpoint").iterdir())
+    M.main(common + ["--split", "val", "--load_dir", str(run), "--checkepoch", "1", "--checkpoint",
+                           ck.name.split("_")[-1][:-4], "--checksession", "0", "INTER", "--load_coarse"])
+    assert "Epoch [1/1][1/2]" in (run / "experiment_train.log").read_text()
+    assert "Evaluation" in (run / "experiment_val.log").read_text()
