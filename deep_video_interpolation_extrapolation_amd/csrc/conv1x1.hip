@@ -2,13 +2,15 @@
 // (forward 1x1 convs of HRNet's bottlenecks / fuse layers, and the data gradient of 1x1 convs,
 // including the 1x1 stride phases of strided data gradients through the output placement).
 //
-// A 1x1 conv needs no spatial tiling: a workgroup owns 256 consecutive pixels and BC output
-// channels (BC = 32*TMC up to 256, so 448-channel layers take two column tiles) and walks the
-// input channels in 64-channel K-steps.  Both operands are staged by LDS-DMA into 128-byte
-// XOR-swizzled rows (x tile 256 x 128 B, weight tile BC x 128 B), two stages in flight.
-// Eight waves each own 32 pixels x BC channels (TMC accumulators of 32x32): per 16-deep
-// k-slice a wave reads one pixel fragment and TMC weight fragments and issues TMC MFMAs
-// (v_mfma_f32_32x32x16_bf16).  Epilogue from registers (permlane32 pairing to 16-byte rows)
+// A 1x1 conv needs no spatial tiling: a workgroup owns BP consecutive pixels and BC output
+// channels (448-channel layers take two 256-channel column tiles) and walks the input
+// channels in K-steps of KC channels.  Both operands are staged by LDS-DMA into XOR-swizzled
+// rows (x tile BP x 2KC bytes, weight tile BC x 2KC bytes), NS stages in the ring.  The
+// waves form an NWP x NWC grid; each owns 32*MI pixels x 32*TMC channels (MI*TMC
+// accumulators of 32x32): per 16-deep k-slice it reads MI pixel fragments and TMC weight
+// fragments from LDS and issues MI*TMC MFMAs (v_mfma_f32_32x32x16_bf16).  LDS reads bound
+// the wide layers, so the 64-pixel x 128-channel wave tile (6 fragments per 8 MFMAs) beats
+// the 32 x 224 one (8 per 7) even though it pads 448 channels to 512.  Epilogue from registers (permlane32 pairing to 16-byte rows)
 // with bias / residual / accumulate / activation / activation-derivative fused.
 //
 // Reference op replaced: nn.Conv2d(kernel_size=1) forward and backward-data (nets/HRNet.py
@@ -63,21 +65,34 @@ __device__ __forceinline__ void unpack8(const i32x4 t, float* v) {
   }
 }
 
-template <int TMC, int NS>
+// KC = input channels per K-step (64: 128-byte LDS rows, 32: 64-byte rows, half the stage
+// bytes, so the same LDS holds twice the stages in flight).  A DMA piece is always 1 KB:
+// RPP rows of RB bytes.
+// Wave grid: NWP x NWC waves; a wave owns 32*MI pixels x 32*TMC channels (MI*TMC
+// accumulators of 32x32), so per 16-deep k-slice it reads MI + TMC fragments for MI*TMC MFMAs.
+template <int TMC, int NS, int KC, int NWP, int MI = 1, int NWC = 1>
 struct G1Cfg {
-  static constexpr int BC = 32 * TMC;
-  static constexpr int BP = 256;
-  static constexpr int XSZ = BP * 128;  // 32 pieces
-  static constexpr int WSZ = BC * 128;  // BC/8 pieces
+  static constexpr int NW = NWP * NWC;
+  static constexpr int BC = 32 * TMC * NWC;
+  static constexpr int BP = 32 * MI * NWP;
+  static constexpr int RB = KC * 2;              // LDS row bytes
+  static constexpr int NCH = RB / 16;            // 16-byte chunks per row (8 or 4)
+  static constexpr int RPP = 64 / NCH;           // rows per 1 KB piece (8 or 16)
+  static constexpr int NSL = KC / 16;            // 16-deep MFMA k-slices per K-step
+  static constexpr int XSZ = BP * RB;
+  static constexpr int WSZ = BC * RB;
   static constexpr int STAGE = XSZ + WSZ;
   static constexpr int SMEM = NS * STAGE;  // NS stages: NS-1 K-steps in flight
-  static constexpr int XQ = BP / 8 / 8;           // x pieces per wave (8 waves)
-  static constexpr int WQ = (BC / 8 + 7) / 8;     // weight pieces per wave (upper bound)
+  static constexpr int XQ = BP / RPP / NW;            // x pieces per wave
+  static constexpr int WQ = (BC / RPP + NW - 1) / NW;  // weight pieces per wave (upper bound)
+  // chunk swizzle: the 16 rows one ds_read_b128 pass touches land on distinct banks
+  static __device__ __forceinline__ int swz(int row) { return NCH == 8 ? (row >> 1) & 7 : (row >> 2) & 3; }
 };
 
-template <int TMC, int NS, bool OUTF32>
-__global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, int n_ct, int n_tiles) {
-  typedef G1Cfg<TMC, NS> C;
+template <int TMC, int NS, int KC, int NWP, int MI, int NWC, bool OUTF32>
+__global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv_desc p, int n_ct, int n_tiles) {
+  typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
+  constexpr int NW = C::NW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -91,24 +106,24 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
   const int c0 = (bid % n_ct) * C::BC;
   const int p0 = (bid / n_ct) * C::BP;
   const int npix = p.n * p.oh * p.ow;
-  const int nk = (p.c + 63) >> 6;
+  const int nk = (p.c + KC - 1) / KC;
 
-  // DMA lane geometry: piece = 8 rows x 128 B; lane -> row 8*piece + (lane>>3), LDS chunk
-  // (lane & 7) holding source chunk (lane & 7) ^ swz(row), swz(row) = (row >> 1) & 7
-  const int lrow = lane >> 3, lch = lane & 7;
+  // DMA lane geometry: piece = RPP rows x RB bytes; lane -> row RPP*piece + lane / NCH, LDS
+  // chunk (lane % NCH) holding source chunk (lane % NCH) ^ swz(row)
+  const int lrow = lane / C::NCH, lch = lane % C::NCH;
   unsigned xo[C::XQ];
 #pragma unroll
   for (int q = 0; q < C::XQ; ++q) {
-    const int row = (wave + 8 * q) * 8 + lrow;
-    const int cs = lch ^ ((row >> 1) & 7);
+    const int row = (wave + NW * q) * C::RPP + lrow;
+    const int cs = lch ^ C::swz(row);
     xo[q] = (p0 + row < npix) ? (unsigned)(p0 + row) * (unsigned)p.x_ld * 2u + cs * 16u : OOB;
     if (cs * 8 >= p.c) xo[q] = OOB;  // (c < 64: channel padding)
   }
   unsigned wo[C::WQ];
 #pragma unroll
   for (int q = 0; q < C::WQ; ++q) {
-    const int row = (wave + 8 * q) * 8 + lrow;
-    const int cs = lch ^ ((row >> 1) & 7);
+    const int row = (wave + NW * q) * C::RPP + lrow;
+    const int cs = lch ^ C::swz(row);
     wo[q] = (row < C::BC && cs * 8 < p.c) ? (unsigned)row * (unsigned)p.kpad * 2u + cs * 16u : OOB;
   }
   const unsigned long long xbytes =
@@ -118,47 +133,50 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
   auto stage = [&](int k, int sb) {
     char* X = smem + sb * C::STAGE;
     char* W = X + C::XSZ;
-    // K-step k: channels 64k .. 64k+63 (chunks past c land as zeros: range check below)
-    const int xr = (int)(xbytes - (unsigned long long)k * 128);
+    // K-step k: channels KC*k .. KC*k+KC-1 (chunks past c land as zeros: range check below)
+    const int xr = (int)(xbytes - (unsigned long long)k * C::RB);
     const __amdgpu_buffer_rsrc_t rx =
-        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)k * 128), 0, xr, 0x00020000);
-    const unsigned wb = (unsigned)(c0 * p.kpad + 64 * k) * 2u;
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)k * C::RB), 0, xr, 0x00020000);
+    const unsigned wb = (unsigned)(c0 * p.kpad + KC * k) * 2u;
     const __amdgpu_buffer_rsrc_t rw =
         __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + wb), 0, (int)(wbytes - wb), 0x00020000);
-    const int cvalid = p.c - 64 * k;  // channels of this K-step that exist
+    const int cvalid = p.c - KC * k;  // channels of this K-step that exist
 #pragma unroll
     for (int q = 0; q < C::XQ; ++q) {
-      const int row = (wave + 8 * q) * 8 + lrow;
-      const int cs = lch ^ ((row >> 1) & 7);
+      const int row = (wave + NW * q) * C::RPP + lrow;
+      const int cs = lch ^ C::swz(row);
       const unsigned o = cs * 8 < cvalid ? xo[q] : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_1x1)(X + (wave + 8 * q) * 1024), 16, o, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_1x1)(X + (wave + NW * q) * 1024), 16, o, 0, 0, 0);
     }
 #pragma unroll
     for (int q = 0; q < C::WQ; ++q) {
-      if (wave + 8 * q < C::BC / 8) {
-        const int row = (wave + 8 * q) * 8 + lrow;
-        const int cs = lch ^ ((row >> 1) & 7);
+      if (wave + NW * q < C::BC / C::RPP) {
+        const int row = (wave + NW * q) * C::RPP + lrow;
+        const int cs = lch ^ C::swz(row);
         const unsigned o = cs * 8 < cvalid ? wo[q] : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_1x1)(W + (wave + 8 * q) * 1024), 16, o, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_1x1)(W + (wave + NW * q) * 1024), 16, o, 0, 0, 0);
       }
     }
   };
 
-  // fragment addresses: pixel row = wave*32 + r32 (B operand), weight rows 32*j + r32 (A);
-  // k-slice s uses chunk 2s + h
-  int xf[4], wf[4];
+  // fragment addresses: pixel rows wp*32*MI + 32*i + r32 (B operand), weight rows
+  // wc*32*TMC + 32*j + r32 (A); k-slice s uses chunk 2s + h (32-row offsets keep the swizzle)
+  const int wp = wave % NWP, wc = wave / NWP;
+  int xf[C::NSL], wf[C::NSL];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int prow = wave * 32 + r32;
-    xf[s] = prow * 128 + (((2 * s + hh) ^ ((prow >> 1) & 7)) << 4);
-    wf[s] = r32 * 128 + (((2 * s + hh) ^ ((r32 >> 1) & 7)) << 4);  // (+ 32*j rows: same swizzle)
+  for (int s = 0; s < C::NSL; ++s) {
+    const int prow = wp * 32 * MI + r32;
+    xf[s] = prow * C::RB + (((2 * s + hh) ^ C::swz(prow)) << 4);
+    wf[s] = (wc * 32 * TMC + r32) * C::RB + (((2 * s + hh) ^ C::swz(r32)) << 4);
   }
 
-  f32x16 acc[TMC];
+  f32x16 acc[MI][TMC];
 #pragma unroll
-  for (int j = 0; j < TMC; ++j)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    for (int j = 0; j < TMC; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   // prologue: K-steps 0 .. NS-2 in flight
 #pragma unroll
@@ -168,18 +186,23 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
     const int sb = k % NS;
     // stage k has landed for every wave: this wave's own pieces by the counted wait (stage
     // k+1, issued after it, may stay in flight), the other waves' by the barrier
-    if constexpr (NS == 3) {
+    if constexpr (NS >= 3) {
+      // stages k+1 .. k+NS-2 were issued after stage k: that many may stay in flight
+      static_assert(NS <= 5, "wait table covers up to 3 stages in flight");
       constexpr int P_HI = C::XQ + C::WQ, P_LO = C::XQ + C::WQ - 1;  // pieces per wave per stage
-      if (k + 1 < nk) {
-        if (wave + 8 * (C::WQ - 1) < C::BC / 8)
-          DVIE_VMCNT1(P_HI);
-        else
-          DVIE_VMCNT1(P_LO);
+      static_assert(3 * P_HI < 64, "vmcnt is 6 bits");
+      const bool hi = wave + NW * (C::WQ - 1) < C::BC / C::RPP;
+      const int m = min(NS - 2, nk - 1 - k);
+      if (m >= 3) {
+        if (hi) DVIE_VMCNT1(3 * P_HI); else DVIE_VMCNT1(3 * P_LO);
+      } else if (m == 2) {
+        if (hi) DVIE_VMCNT1(2 * P_HI); else DVIE_VMCNT1(2 * P_LO);
+      } else if (m == 1) {
+        if (hi) DVIE_VMCNT1(P_HI); else DVIE_VMCNT1(P_LO);
       } else {
         __builtin_amdgcn_s_waitcnt(0);
       }
     } else {
-      static_assert(NS <= 2, "NS > 3 needs a deeper wait table");
       __builtin_amdgcn_s_waitcnt(0);
     }
     __builtin_amdgcn_s_barrier();
@@ -187,21 +210,26 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
     const char* X = smem + sb * C::STAGE;
     const char* W = X + C::XSZ;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const i32x4 b = *(const i32x4*)(X + xf[s]);
-      i32x4 a[TMC];
+    for (int s = 0; s < C::NSL; ++s) {
+      i32x4 b[MI], a[TMC];
 #pragma unroll
-      for (int j = 0; j < TMC; ++j) a[j] = *(const i32x4*)(W + wf[s] + j * 32 * 128);
+      for (int i = 0; i < MI; ++i) b[i] = *(const i32x4*)(X + xf[s] + i * 32 * C::RB);
 #pragma unroll
-      for (int j = 0; j < TMC; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[j]), __builtin_bit_cast(bf16x8, b),
-                                                         acc[j], 0, 0, 0);
+      for (int j = 0; j < TMC; ++j) a[j] = *(const i32x4*)(W + wf[s] + j * 32 * C::RB);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < TMC; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[j]),
+                                                              __builtin_bit_cast(bf16x8, b[i]), acc[i][j], 0, 0, 0);
     }
   }
 
-  // ---- epilogue: lane owns pixel wave*32 + r32; after permlane32 pairing, lane half h holds
-  // channels 16P + 8h .. +7 of pair P of each 32-channel accumulator
-  const int pix = p0 + wave * 32 + r32;
+  // ---- epilogue: lane owns pixel wp*32*MI + 32*i + r32; after permlane32 pairing, lane half h
+  // holds channels 16P + 8h .. +7 of pair P of each 32-channel accumulator
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+  const int pix = p0 + wp * 32 * MI + 32 * i + r32;
   float v[TMC][2][8];
 #pragma unroll
   for (int j = 0; j < TMC; ++j)
@@ -209,12 +237,12 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
     for (int P = 0; P < 2; ++P)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[j][8 * P + e]),
-                                                         __float_as_uint(acc[j][8 * P + 4 + e]), false, false);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * P + e]),
+                                                         __float_as_uint(acc[i][j][8 * P + 4 + e]), false, false);
         v[j][P][e] = __uint_as_float(sw[0]);
         v[j][P][4 + e] = __uint_as_float(sw[1]);
       }
-  if (pix >= npix) return;
+  if (pix >= npix) continue;
   long long yp = pix;
   if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) {
     const int hw = p.oh * p.ow;
@@ -226,7 +254,7 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
   for (int j = 0; j < TMC; ++j)
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
-      const int co = c0 + 32 * j + 16 * P + 8 * hh;
+      const int co = c0 + wc * 32 * TMC + 32 * j + 16 * P + 8 * hh;
       if (co >= p.cout) continue;
       float* w = v[j][P];
       if (p.bias) {
@@ -288,18 +316,20 @@ __global__ __launch_bounds__(512) void conv1x1_kernel(const dvie_conv_desc p, in
         *(i32x4*)dst = o;
       }
     }
+  }
 }
 
-template <int TMC, int NS>
+template <int TMC, int NS, int KC = 64, int NWP = 8, int MI = 1, int NWC = 1>
 static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
-  typedef G1Cfg<TMC, NS> C;
+  typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
+  constexpr int NW = C::NW;
   const int npix = p.n * p.oh * p.ow;
   const int n_ct = (p.cout + C::BC - 1) / C::BC;
   const int n_tiles = n_ct * ((npix + C::BP - 1) / C::BP);
   if (p.out_f32)
-    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, true>), dim3(n_tiles), dim3(512), 0, s, p, n_ct, n_tiles);
+    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, true>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
   else
-    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, false>), dim3(n_tiles), dim3(512), 0, s, p, n_ct, n_tiles);
+    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
 }
 
 // Returns true when the 1x1 GEMM kernel took the launch.
@@ -314,13 +344,27 @@ bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (cfg >= 0 && cfg < 100) return false;  // tuning override forces the halo / per-tap kernels
   const int cout = p.cout;
   const bool one = p.c <= 64;  // a single K-step: one stage, several workgroups per CU
-  if (cfg < 0) cfg = cout <= 64 ? 100 : (cout <= 128 || one) ? 101 : 102;
+  // wide layers: 2-D wave grid (116; 448->448 heads 724 -> 662 us, 64->256 166 -> 155 us
+  // at 8x256x512, tools/conv_tune.py)
+  // (DVIE_CONV1X1_WIDE overrides the wide-layer choice alone, for A/B runs of the whole step)
+  static const int wide = getenv("DVIE_CONV1X1_WIDE") && *getenv("DVIE_CONV1X1_WIDE") ? atoi(getenv("DVIE_CONV1X1_WIDE")) : 116;
+  if (cfg < 0) cfg = cout <= 64 ? 100 : cout <= 128 ? 101 : wide;
   switch (cfg) {
     case 100: one ? launch_1x1<2, 1>(p, s) : launch_1x1<2, 3>(p, s); break;
     case 101: one ? launch_1x1<4, 1>(p, s) : launch_1x1<4, 3>(p, s); break;
     case 102: one ? launch_1x1<7, 1>(p, s) : launch_1x1<7, 2>(p, s); break;
     case 103: one ? launch_1x1<8, 1>(p, s) : launch_1x1<8, 2>(p, s); break;
     case 104: one ? launch_1x1<4, 1>(p, s) : launch_1x1<4, 2>(p, s); break;
+    // 32-channel K-steps: deeper pipelines in the same LDS (measured: no gain, the kernel is
+    // not load-latency bound)
+    case 105: one ? launch_1x1<7, 1>(p, s) : launch_1x1<7, 4, 32>(p, s); break;
+    case 106: one ? launch_1x1<7, 1>(p, s) : launch_1x1<7, 5, 32>(p, s); break;
+    // 4-wave workgroups (128-pixel tiles, two workgroups per CU)
+    case 110: one ? launch_1x1<7, 1, 64, 4>(p, s) : launch_1x1<7, 2, 32, 4>(p, s); break;
+    // 2-D wave grids: 64-pixel x 128-channel wave tiles (6 fragments per 8 MFMAs)
+    case 116: one ? launch_1x1<4, 1, 64, 4, 2, 2>(p, s) : launch_1x1<4, 2, 64, 4, 2, 2>(p, s); break;
+    case 118: one ? launch_1x1<2, 1, 64, 4, 2, 2>(p, s) : launch_1x1<2, 3, 64, 4, 2, 2>(p, s); break;
+    case 119: one ? launch_1x1<4, 1, 64, 4, 2, 2>(p, s) : launch_1x1<4, 4, 32, 4, 2, 2>(p, s); break;
     default: return false;
   }
   return true;
