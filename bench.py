@@ -32,8 +32,13 @@ KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwis
               8: "batchnorm_fwd", 9: "batchnorm_bwd", 10: "head_fwd", 11: "head_bwd"}
 # HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
 # this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01c_pmc", "traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01zc_pmc", "traffic.json")
 
+
+
+class _StderrLog:
+    def info(self, msg):
+        print(msg, file=sys.stderr, flush=True)
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -174,6 +179,7 @@ def main():
     args = default_args("INTER", syn_type="inter", mode="xs2xs", interval=5, vid_length=1, train_coarse=True,
                         batch_size=a.batch * world, input_h=a.height, input_w=a.width, precision=a.precision,
                         synthetic=a.batch * world, num_workers=0, split="train", rank=rank, gpus=world)
+    args.logger = _StderrLog()  # stdout carries the one JSON line only
     torch.manual_seed(args.seed)
     trainer = InterTrainer(args)
     data = make_batch(a.batch, a.height, a.width, dev, rank * a.batch)
@@ -240,7 +246,7 @@ def main():
             traffic = round(t["bytes_per_launch"]) if t else None
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                 "traffic": traffic, "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE, "
-                                                     "profiles/r01c_pmc)",
+                                                     "profiles/r01zc_pmc)",
                 "algorithmic_bytes_per_launch": round(by / max(1, n)),
                 "kernel": "conv fwd+dgrad family (conv_halo / conv_ws / conv1x1 / conv_igemm kernels)",
                 "launches_per_step": n // max(1, a.profile_steps),

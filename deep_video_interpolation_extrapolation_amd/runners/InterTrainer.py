@@ -230,6 +230,11 @@ class InterTrainer:
             self.model.module.coarse_model.load_state_dict(sd)
         if a.split == "train" and getattr(a, "train_coarse", False) and "coarse_opt" in ckpt:
             self.coarse_opt.load_state_dict(ckpt["coarse_opt"])
+        # epoch bookkeeping as the reference (l.953-958): the file's epoch is checkepoch + 1
         if getattr(a, "resume", False):
+            assert ckpt["epoch"] - 1 == a.checkepoch, [ckpt["epoch"], a.checkepoch]
             self.epoch = ckpt["epoch"]
+        elif a.split != "train":
+            assert ckpt["epoch"] - 1 == a.checkepoch, [ckpt["epoch"], a.checkepoch]
+            self.epoch = ckpt["epoch"] - 1
         self.log.info("checkpoint loaded")
