@@ -176,6 +176,18 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
     case DVIE_EW_COPY:
       VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, v);
       break;
+    case DVIE_EW_IM2COL: {
+      const int t = c / p.ext_c, ch = c - t * p.ext_c;
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] = 0.f;
+      if (t < p.sh0 * p.sw0) {
+        const int ty = t / p.sw0, tx = t - ty * p.sw0;
+        const int Y = y + p.sh1 + ty * p.sh2, X = x + p.sw1 + tx * p.sw2;
+        if (Y >= 0 && Y < p.h && X >= 0 && X < p.w)
+          VecN<T, VW>::load((const T*)p.src0 + (((long long)n * p.h + Y) * p.w + X) * p.src_ld0 + ch, v);
+      }
+      break;
+    }
     case DVIE_EW_L1SIGN: {
       float a[VW], b[VW];
       VecN<T, VW>::load((const T*)p.src0 + pix * p.src_ld0 + c, a);
@@ -261,6 +273,10 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
   if (d->op == DVIE_EW_NCHW || d->op == DVIE_EW_TONCHW || d->op == DVIE_EW_MASK)
     DVIE_CHECK_ARG(d->ext != nullptr, "ew: ext");
   if (d->dact) DVIE_CHECK_ARG(d->z != nullptr && d->z_ld % 4 == 0, "ew: z");
+  if (d->op == DVIE_EW_IM2COL)
+    DVIE_CHECK_ARG(d->ext_c > 0 && d->ext_c % 8 == 0 && d->src0 && d->src_ld0 >= d->ext_c &&
+                       d->sh0 > 0 && d->sw0 > 0 && d->sh0 * d->sw0 * d->ext_c <= d->c,
+                   "ew: im2col ext_c=%d c=%d taps=%dx%d", d->ext_c, d->c, d->sh0, d->sw0);
   DVIE_CHECK_ARG((long long)d->n * d->h < 65536 && (long long)d->w * d->c < (1LL << 30), "ew: grid too large");
   hipStream_t s = (hipStream_t)stream;
   // 16-byte vectors for bf16 when every operand allows it

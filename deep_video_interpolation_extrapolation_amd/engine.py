@@ -967,6 +967,9 @@ class Plan:
 
             def em(beta, res, res_ld, dact, z, z_ld, phases=phases, x=x, xg=xg, out=out, gout=gout, gld=gld, lay=lay):
                 ops = []
+                if self._im2col_dgrad(lay, x, phases):
+                    return self._im2col_dgrad_ops(lay, x, xg, out, gout, gld, phases[0], res, res_ld, z, z_ld, dact,
+                                                  beta)
                 for ph, wt, kpad in phases:
                     o = self.conv_desc(
                         gout, gld, nb, out.H, out.W, lay.cout_p, wt.data_ptr(), kpad, x.c, ph["oh"], ph["ow"], 1, 1,
@@ -983,6 +986,46 @@ class Plan:
                 return ops
 
             self._contrib(x, em)
+
+    def _im2col_dgrad(self, lay, x, phases):
+        """Narrow-input stride-1 data gradients (HRNet's 3x3 448->3 / 448->20 heads: the
+        output gradient has 8 / 24 channels) run as im2col + 1x1 GEMM over K = 9*c (128 /
+        256) instead of the halo kernel's 9 taps x 64 padded channels (bf16 only).  Opt-in
+        (DVIE_IM2COL_DGRAD=1): measured at 8x256x512 the 448->3 head goes 0.838 -> 0.756 ms
+        but the 448->20 head 0.847 -> 0.942 ms (im2col 0.16 ms + GEMM 0.78 ms), no net gain:
+        the GEMM's 448-channel output + activation-derivative read, not the padded MFMA work,
+        bound these layers."""
+        if self.dtype != torch.bfloat16 or os.environ.get("DVIE_IM2COL_DGRAD", "0") != "1":
+            return False
+        if lay.stride != 1 or len(phases) != 1:
+            return False
+        ph, _, kpad = phases[0]
+        return (ph["th"] * ph["tw"] > 1 and lay.cout_p % 8 == 0 and lay.cout_p <= 32 and x.c >= 128
+                and kpad % 64 == 0 and ph["ry"] == 0 and ph["rx"] == 0)
+
+    def _im2col_dgrad_ops(self, lay, x, xg, out, gout, gld, phase, res, res_ld, z, z_ld, dact, beta):
+        ph, wt, kpad = phase
+        nb = self.nb
+        npx = nb * ph["oh"] * ph["ow"]
+        buf = getattr(self, "_i2c", None)
+        if buf is None or buf.numel() < npx * kpad:  # one scratch for all such layers (one stream)
+            buf = torch.empty(npx * kpad, dtype=self.dtype, device=self.device)
+            self._i2c = buf
+            self.keep.append(buf)
+        e = self.ew_desc(L.EW_IM2COL, nb, out.H, out.W, kpad, buf.data_ptr(), kpad,
+                         srcs=[(gout, gld, ph["th"], ph["tw"]), (None, 0, ph["dy0"], ph["dx0"]),
+                               (None, 0, ph["ddy"], ph["ddx"])])
+        e.u.ew.nsrc, e.u.ew.ext_c = 1, lay.cout_p
+        e.meta = dict(cls="pointwise", name=lay.name + ".im2col", flops=0.0,
+                      bytes=float(self.es * npx * (lay.cout_p + kpad)))
+        one = dict(th=1, tw=1, dy0=0, dx0=0, ddy=1, ddx=1)
+        o = self.conv_desc(buf.data_ptr(), kpad, nb, out.H, out.W, kpad, wt.data_ptr(), kpad, x.c, ph["oh"], ph["ow"],
+                           1, 1, one, xg, x.buf.C, x.H, x.W, res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact,
+                           beta=beta)
+        o.meta = dict(cls="conv_dgrad", name=lay.name, flops=2.0 * npx * lay.cin * lay.cout * ph["th"] * ph["tw"],
+                      bytes=float(self.es * (npx * kpad + npx * lay.cin * (1 + (res is not None) + (z is not None)
+                                                                            + beta) + lay.cout * lay.cin * 9)))
+        return [e, o]
 
     def _convT_backward(self, op, gout, gld):
         """nn.ConvTranspose2d backward through its virtual conv (see ConvLayer): the input

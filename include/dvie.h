@@ -187,6 +187,11 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
  *  DVIE_EW_MASK   y = src_0 * m or src_0 * (1 - m) (ext_c = 0 / 1), m = ext[n, 0, y, x]
  *                 (fp32, NCHW strides): the fg/bg split of nets/SepUNet.py:45-46 (its own
  *                 adjoint with respect to src_0).
+ *  DVIE_EW_IM2COL y[n,y,x][t*ext_c + ch] = src_0[n, y + sh1 + ty*sh2, x + sw1 + tx*sw2][ch]
+ *                 for tap t = ty*sw0 + tx of an sh0 x sw0 tap grid; zero outside the (h, w)
+ *                 image and for t >= sh0*sw0 (ext_c % 8 == 0).  Lowers a stride-1 conv whose
+ *                 input has few channels (the data gradient of HRNet's 3x3 448->3 / 448->20
+ *                 heads) to a 1x1 GEMM over K = taps*ext_c instead of taps*64.
  * then the shared epilogue: v += res; v += y_old (beta); v = act(v); v *= act'(z); y = v.
  * Channels c % 4 == 0; all lds % 4 == 0.
  */
@@ -199,6 +204,7 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
 #define DVIE_EW_NCHW 6
 #define DVIE_EW_TONCHW 7
 #define DVIE_EW_MASK 8
+#define DVIE_EW_IM2COL 9
 
 typedef struct dvie_ew_desc {
   void* y;
