@@ -54,3 +54,26 @@ def test_clip_store_option_and_no_cpu_fallback(tmp_path):
     np.savez(store, imgs=np.zeros((2, 3, 8, 8, 3), np.uint8), segs=np.zeros((2, 3, 8, 8), np.uint8))
     with pytest.raises(L.DvieError):
         load_clip_store(str(store), "train", (4, 4), torch.device("cpu"))
+
+
+def test_device_loader_rank_shards_partition_epoch():
+    """DeviceClips.epoch / DeviceClipLoader index logic (host side, no GPU): for each epoch
+    the ranks' shards are disjoint, cover n - n % world clips, follow a permutation seeded
+    by seed + epoch, and every rank runs the same number of batches."""
+    from deep_video_interpolation_extrapolation_amd.data import DeviceClipLoader, DeviceClips
+    dc = DeviceClips.__new__(DeviceClips)
+    dc.n = 11
+    dc.batch = lambda idx: {"idx": list(int(i) for i in idx)}
+    for ep in (0, 3):
+        shards = []
+        for r in range(3):
+            ld = DeviceClipLoader(dc, 2, rank=r, world=3, shuffle=True, seed=7)
+            ld.set_epoch(ep)
+            got = [i for b in ld for i in b["idx"]]
+            assert len(list(iter(ld))) == len(ld) == 1
+            shards.append(got)
+        perm = np.random.RandomState(7 + ep).permutation(11)
+        for r in range(3):
+            assert shards[r] == list(perm[r::3][:3][:2])
+        flat = [i for s in shards for i in s]
+        assert len(set(flat)) == len(flat)
