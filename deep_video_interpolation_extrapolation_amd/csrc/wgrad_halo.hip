@@ -63,11 +63,11 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
   return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + i;
 }
 
-// 8 waves: (co half, ci half, row half); the two row halves accumulate separately and write
-// two partial slabs per split.
+// 8 waves: (co half, ci half, row half); the two row halves accumulate separately and are
+// summed through LDS into one partial slab per split.
 template <int TH, int TW, int PR, int TMO, int TMI>
 __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
-                                                         int tiles_x, int tiles_y, int n_tiles) {
+                                                         int tiles_x, int tiles_y, int n_tiles, int merge) {
   typedef WgCfg<TH, TW, PR, TMO, TMI> C;
   static_assert(PR % 2 == 0, "row halves");
   constexpr int NW = 8;
@@ -242,24 +242,43 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
   }
 
   // ---- partial slab ws[split][co][t*c + ci] ----
+  // The two row halves are summed through LDS first (one slab per split: half the slab
+  // writes and half the reduction's reads).  Per tap, the wrow = 1 waves park their
+  // accumulators lane-fastest (conflict-free), the wrow = 0 partner adds and stores.
   // C layout: column (ci) = lane & 31, rows (co) = 8*(e>>2) + 4*(lane>>5) + (e&3)
   const long long ws_k = (long long)C::NT * p.c;
   const int r32 = lane & 31, hh = lane >> 5;
-  float* slab = p.ws + (long long)(2 * split + wrow) * p.cout * ws_k;
+  float* slab = p.ws + (long long)(merge ? split : 2 * split + wrow) * p.cout * ws_k;
+  static_assert(4 * TMO * TMI * 16 * 64 * 4 <= C::SMEM, "row-half exchange fits the LDS");
+  float* X = (float*)smem + (wco * 2 + wci) * (TMO * TMI * 16 * 64) + lane;
 #pragma unroll
-  for (int t = 0; t < C::NT; ++t)
+  for (int t = 0; t < C::NT; ++t) {
+    if (merge && wrow == 1) {
 #pragma unroll
-    for (int jo = 0; jo < TMO; ++jo)
+      for (int j = 0; j < TMO * TMI; ++j)
 #pragma unroll
-      for (int ji = 0; ji < TMI; ++ji) {
-        const int ci = k0 + wci * 32 * TMI + 32 * ji + r32;
-        if (ci >= p.c) continue;
+        for (int e = 0; e < 16; ++e) X[(j * 16 + e) * 64] = acc[t * TMO * TMI + j][e];
+    }
+    if (merge) __syncthreads();
+    if (!merge || wrow == 0) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int co = c0 + wco * 32 * TMO + 32 * jo + 8 * (e >> 2) + 4 * hh + (e & 3);
-          if (co < p.cout) slab[(long long)co * ws_k + (long long)t * p.c + ci] = acc[(t * TMO + jo) * TMI + ji][e];
+      for (int jo = 0; jo < TMO; ++jo)
+#pragma unroll
+        for (int ji = 0; ji < TMI; ++ji) {
+          const int ci = k0 + wci * 32 * TMI + 32 * ji + r32;
+          if (ci >= p.c) continue;
+          const int j = jo * TMI + ji;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int co = c0 + wco * 32 * TMO + 32 * jo + 8 * (e >> 2) + 4 * hh + (e & 3);
+            if (co < p.cout)
+              slab[(long long)co * ws_k + (long long)t * p.c + ci] =
+                  acc[t * TMO * TMI + j][e] + (merge ? X[(j * 16 + e) * 64] : 0.f);
+          }
         }
-      }
+    }
+    if (merge) __syncthreads();
+  }
 }
 
 static bool wgrad_halo_eligible(const dvie_wgrad_desc& p) {
@@ -308,8 +327,11 @@ int wgrad_halo_splits(const dvie_wgrad_desc& p) {
   return s < 1 ? 1 : s;
 }
 
-// two partial slabs per split (the two row halves of each workgroup)
-int wgrad_halo_slabs(const dvie_wgrad_desc& p) { return wgrad_halo_eligible(p) ? 2 * p.splits : p.splits; }
+// one partial slab per split (the kernel sums its two row halves)
+// DVIE_WG_MERGE=0: two slabs per split, row halves unmerged (A/B runs)
+static const int wg_merge = getenv("DVIE_WG_MERGE") && *getenv("DVIE_WG_MERGE") == '0' ? 0 : 1;
+
+int wgrad_halo_slabs(const dvie_wgrad_desc& p) { return wgrad_halo_eligible(p) && !wg_merge ? 2 * p.splits : p.splits; }
 
 bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   if (!wgrad_halo_eligible(p)) return false;
@@ -319,7 +341,7 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   const int grid = n_co * n_ci * p.splits;
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
   hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
-                     tiles_x, tiles_y, n_tiles)
+                     tiles_x, tiles_y, n_tiles, wg_merge)
   if (p.th == 3)
     DVIE_WG(3, 4, 1, 1);
   else if (w.tmo == 2 && w.tmi == 2)
