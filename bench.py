@@ -160,10 +160,35 @@ def clip_prep_roofline(dev, n, H, W, reps=20):
             "note": "per batch call incl. its small host->device index/param copies and output allocation"}
 
 
+def launch_command(a, argv, port):
+    """`bench.py --gpus N` (N > 1) started as a plain process: the torchrun command that
+    runs it as N ranks, one per GPU (the reference's one-process-per-GPU launch,
+    main.py:133-154, which mp.spawn's `gpus` workers)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # nothing has touched the GPU yet: run the N ranks as a child torchrun and exit with
+        # its status (never exec from here)
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(launch_command(a, sys.argv[1:], _free_port()), env=env))
     os.environ["DVIE_PRECISION"] = a.precision
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == a.gpus or a.gpus == 1, f"--gpus {a.gpus} but WORLD_SIZE={world}"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -383,17 +383,32 @@ extern "C" int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
   DVIE_CHECK_ARG(((uintptr_t)d->x & 15) == 0 && ((uintptr_t)d->w & 15) == 0 && ((uintptr_t)d->y & 15) == 0,
                  "conv: x/w/y not 16B aligned");
   DVIE_CHECK_ARG(!d->bias || ((uintptr_t)d->bias & 15) == 0, "conv: bias not 16B aligned");
-  const unsigned long long xb = (unsigned long long)d->n * d->ih * d->iw * d->x_ld * es;
+  DVIE_CHECK_ARG(d->dtype == DVIE_BF16 || d->out_f32 || d->dtype == DVIE_F32, "conv: dtype");
+  // The kernels address the input (and weights) through buffer resources with 32-bit
+  // offsets.  A larger input is run as batch chunks whose input span fits: the images of
+  // a batch are independent, so each chunk is the same conv over n' images with x / y /
+  // res / z advanced by n0 images (the output keeps its own geometry yh x yw).
+  const unsigned long long img_x = (unsigned long long)d->ih * d->iw * d->x_ld * es;
   const unsigned long long wb = (unsigned long long)d->cout * d->kpad * es;
-  DVIE_CHECK_ARG(xb < 0xFFFFFF00ull && wb < 0xFFFFFF00ull, "conv: operand exceeds the 4 GiB buffer range");
+  DVIE_CHECK_ARG(wb < 0xFFFFFF00ull, "conv: weights exceed the 4 GiB buffer range");
+  DVIE_CHECK_ARG(img_x < 0xFFFFFF00ull, "conv: one input image exceeds the 4 GiB buffer range");
   hipStream_t s = (hipStream_t)stream;
-  if (conv1x1_launch(*d, s)) DVIE_RETURN_LAUNCH();
-  if (conv_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();
-  if (d->dtype == DVIE_BF16)
-    dispatch_conv<bf16_t>(*d, s);
-  else {
-    DVIE_CHECK_ARG(d->out_f32 || d->dtype == DVIE_F32, "conv: dtype");
-    dispatch_conv<float>(*d, s);
+  const long long chunk = (long long)(0xFFFFFF00ull / img_x) < d->n ? (long long)(0xFFFFFF00ull / img_x) : d->n;
+  const int oes = (d->out_f32 || d->dtype == DVIE_F32) ? 4 : 2;
+  const unsigned long long img_y = (unsigned long long)d->yh * d->yw;
+  for (long long n0 = 0; n0 < d->n; n0 += chunk) {
+    dvie_conv_desc c = *d;
+    c.n = (int)(d->n - n0 < chunk ? d->n - n0 : chunk);
+    c.x = (const char*)d->x + n0 * img_x;
+    c.y = (char*)d->y + n0 * img_y * d->y_ld * oes;
+    if (d->res) c.res = (const char*)d->res + n0 * img_y * d->res_ld * oes;
+    if (d->z) c.z = (const char*)d->z + n0 * img_y * d->z_ld * es;
+    if (conv1x1_launch(c, s)) continue;
+    if (conv_halo_launch(c, s)) continue;
+    if (c.dtype == DVIE_BF16)
+      dispatch_conv<bf16_t>(c, s);
+    else
+      dispatch_conv<float>(c, s);
   }
   DVIE_RETURN_LAUNCH();
 }

@@ -755,6 +755,9 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (!t1 && !t3 && !t22 && !t12 && !t21) return false;
   const unsigned long long pix = (unsigned long long)p.n * p.ih * p.iw;
   if (pix >= (1ull << 31)) return false;
+  // 32-bit halo offsets: the input's byte span must fit (dvie_conv2d_fwd rejects larger
+  // inputs for every kernel; kept here so the halo path never relies on the caller)
+  if (((pix - 1) * (unsigned long long)p.x_ld + (unsigned long long)p.c) * 2ull >= 0xFFFFFF00ull) return false;
   int cfg = env_cfg();
   if (cfg == -1) return false;
   if (t3 && p.c <= 64 && p.cout <= 64 && (cfg == -3 || cfg == 8) && (long long)p.n * p.oh * p.ow >= 65536) {

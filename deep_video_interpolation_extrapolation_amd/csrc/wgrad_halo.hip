@@ -281,16 +281,24 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
   }
 }
 
+// diagnostic override, read once (plan-time slab counts and launches must agree):
+// DVIE_WGRAD_HALO=0 = per-tap kernel only
+static const bool wg_halo_env_off = getenv("DVIE_WGRAD_HALO") && *getenv("DVIE_WGRAD_HALO") == '0';
+
 static bool wgrad_halo_eligible(const dvie_wgrad_desc& p) {
   if (p.dtype != DVIE_BF16) return false;
-  const char* e = getenv("DVIE_WGRAD_HALO");  // diagnostic override: 0 = per-tap kernel only
-  if (e && *e == '0') return false;
+  if (wg_halo_env_off) return false;
   if (p.sy != 1 || p.sx != 1 || p.ddy != 1 || p.ddx != 1) return false;
   if (!((p.th == 1 && p.tw == 1) || (p.th == 3 && p.tw == 3))) return false;
   if (p.c % 8 != 0 || p.cout % 8 != 0) return false;
   if (p.g_ld % 8 != 0 || p.x_ld % 8 != 0) return false;
-  if ((unsigned long long)p.n * p.ih * p.iw >= (1ull << 31) || (unsigned long long)p.n * p.oh * p.ow >= (1ull << 31))
-    return false;
+  const unsigned long long npx = (unsigned long long)p.n * p.ih * p.iw, npg = (unsigned long long)p.n * p.oh * p.ow;
+  if (npx >= (1ull << 31) || npg >= (1ull << 31)) return false;
+  // the kernel forms 32-bit buffer offsets: both operands' byte spans must fit (else the
+  // per-tap kernel, 64-bit addressing, takes the launch)
+  const unsigned long long xspan = ((npx - 1) * (unsigned long long)p.x_ld + (unsigned long long)p.c) * 2ull;
+  const unsigned long long gspan = ((npg - 1) * (unsigned long long)p.g_ld + (unsigned long long)p.cout) * 2ull;
+  if (xspan >= 0xFFFFFF00ull || gspan >= 0xFFFFFF00ull) return false;
   return true;
 }
 

@@ -175,8 +175,12 @@ class DeviceClipLoader:
     """DataLoader stand-in over `DeviceClips` (the reference's DataLoader + DistributedSampler
     pair, InterTrainer.py:86-96): each rank iterates its rank-strided shard of a permutation
     seeded by the epoch (`set_epoch`, as DistributedSampler.set_epoch), one prepared batch of
-    `batch_size` clips per step, already on the device.  The last partial batch is dropped
-    (every rank runs the same number of steps, so the gradient all-reduce stays matched)."""
+    `batch_size` clips per step, already on the device.  Training (shuffle=True) drops the
+    last partial batch (every rank runs the same number of steps, so the gradient
+    all-reduce stays matched).  Validation (shuffle=False) covers every clip exactly as the
+    reference's val loader does (InterTrainer.py:97-100: DistributedSampler with its
+    defaults -- seed-0 permutation, padded to a multiple of W by wrapping -- and
+    drop_last=False), so metrics average over the same set."""
 
     def __init__(self, clips, batch_size, rank=0, world=1, shuffle=True, seed=0):
         self.clips, self.bs, self.rank, self.world = clips, max(1, batch_size), rank, world
@@ -186,11 +190,17 @@ class DeviceClipLoader:
     def set_epoch(self, epoch):
         self.ep = epoch
 
+    def _val_indices(self):
+        from torch.utils.data.distributed import DistributedSampler
+        return list(DistributedSampler(range(len(self.clips)), num_replicas=self.world, rank=self.rank))
+
     def __len__(self):
-        return (len(self.clips) // self.world) // self.bs
+        if self.shuffle:
+            return (len(self.clips) // self.world) // self.bs
+        return -(-len(self._val_indices()) // self.bs)
 
     def __iter__(self):
         if self.shuffle:
             return self.clips.epoch(self.bs, self.rank, self.world, seed=self.seed + self.ep)
-        mine = np.arange(len(self.clips))[self.rank::self.world][:len(self.clips) // self.world]
-        return (self.clips.batch(mine[s:s + self.bs]) for s in range(0, len(self) * self.bs, self.bs))
+        mine = np.asarray(self._val_indices(), dtype=np.int64)
+        return (self.clips.batch(mine[s:s + self.bs]) for s in range(0, len(mine), self.bs))

@@ -59,6 +59,9 @@ class ExtraTrainer(InterTrainer):
         if nps > 1:
             assert npo == 1, "rollout (num_pred_step > 1) requires num_pred_once == 1 (reference l.252-253)"
         data = batch_to(data, self.device)
+        # a rollout runs HRNet's backward nps times into one flat gradient: reduce it once,
+        # after the last backward (see GradSync.set_overlap)
+        self.model.set_overlap(nps == 1)
         xs2xs = a.mode == "xs2xs"
         loss_dict = OrderedDict()
         last_rgb = torch.cat([data["frame1"], data["frame2"]], dim=1)

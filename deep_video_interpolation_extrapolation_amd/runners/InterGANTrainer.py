@@ -30,6 +30,9 @@ class InterGANTrainer(InterTrainer):
         args.model = getattr(args, "model", "InterGANNet") or "InterGANNet"
         if args.model != "InterGANNet":
             args.model = "InterGANNet"
+        # the discriminator optimizers must exist before a resume loads their state
+        # (reference l.106-139: every optimizer is built, then load_checkpoint)
+        self._defer_load = True
         super().__init__(args)
         a, m = self.args, self.model.module
         if not getattr(a, "train_coarse", False):
@@ -48,6 +51,8 @@ class InterGANTrainer(InterTrainer):
                 self.VideoDisc_DLoss = GANScalarLoss(weight=a.video_disc_disc_weight)
                 self.VideoDisc_GLoss = GANScalarLoss(weight=a.video_disc_gen_weight)
                 self.video_disc_opt = Adam(list(m.video_disc_model.parameters()), lr=a.video_disc_learning_rate)
+        if getattr(a, "resume", False) or (a.split != "train" and not getattr(a, "checkepoch_range", False)):
+            self.load_checkpoint()  # reference l.138-139
 
     def get_input(self, data):
         """reference l.368-374 (interpolation: frames 1, 3 -> 2)"""
@@ -127,20 +132,37 @@ class InterGANTrainer(InterTrainer):
         return name
 
     def load_checkpoint(self):
+        """reference l.940-1059: weights gated by load_coarse / load_frame_disc /
+        load_video_disc, optimizer states by train_* and load_* (train split), then the
+        epoch bookkeeping of a resume / an evaluation split."""
         a = self.args
         name = self._ckpt_name(a.load_model, a.checksession, a.checkepoch, a.checkpoint, a.load_dir or ".")
         self.log.info("Loading checkpoint %s" % name)
         ckpt = torch.load(name, map_location="cpu", weights_only=True)
         m = self.model.module
-        if "coarse_model" in ckpt:
-            m.coarse_model.load_state_dict(ckpt["coarse_model"])
+
+        def merge(module, sd):
+            cur = module.state_dict()
+            cur.update(sd)
+            module.load_state_dict(cur)
+
+        if getattr(a, "load_coarse", False):
+            merge(m.coarse_model, ckpt["coarse_model"])
         for kind in ("frame_disc", "video_disc"):
-            if getattr(a, kind, False) and kind + "_model" in ckpt:
-                getattr(m, kind + "_model").load_state_dict(ckpt[kind + "_model"])
-                if a.split == "train" and hasattr(self, kind + "_opt") and kind + "_opt" in ckpt:
+            if getattr(a, "load_" + kind, False):
+                assert getattr(a, kind, False), "load_%s needs --%s" % (kind, kind)
+                merge(getattr(m, kind + "_model"), ckpt[kind + "_model"])
+        if a.split == "train":
+            if getattr(a, "train_coarse", False) and getattr(a, "load_coarse", False):
+                self.coarse_opt.load_state_dict(ckpt["coarse_opt"])
+            for kind in ("frame_disc", "video_disc"):
+                if getattr(a, "train_" + kind, False) and getattr(a, "load_" + kind, False):
+                    assert getattr(a, kind, False)
                     getattr(self, kind + "_opt").load_state_dict(ckpt[kind + "_opt"])
-        if a.split == "train" and getattr(a, "train_coarse", False) and "coarse_opt" in ckpt:
-            self.coarse_opt.load_state_dict(ckpt["coarse_opt"])
         if getattr(a, "resume", False):
+            assert ckpt["epoch"] - 1 == a.checkepoch, [ckpt["epoch"], a.checkepoch]
             self.epoch = ckpt["epoch"]
+        elif a.split != "train":
+            assert ckpt["epoch"] - 1 == a.checkepoch, [ckpt["epoch"], a.checkepoch]
+            self.epoch = ckpt["epoch"] - 1
         self.log.info("checkpoint loaded")

@@ -86,7 +86,9 @@ class InterTrainer:
                 self.val_loader = torch.utils.data.DataLoader(
                     self.val_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
                     num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
-        if getattr(args, "resume", False) or getattr(args, "load_coarse", False):
+        # (a subclass that builds more optimizers loads after them: _defer_load)
+        if not getattr(self, "_defer_load", False) and (getattr(args, "resume", False)
+                                                        or getattr(args, "load_coarse", False)):
             self.load_checkpoint()
 
     def _device_loader(self, split, shuffle):

@@ -43,11 +43,26 @@ class GradSync:
         self.hooked = [m for m in self.flat_owners if hasattr(m, "_buckets") and not getattr(m, "post_sync", False)]
         self.post = [m for m in self.flat_owners if m not in self.hooked]
         self.works = []
+        self.overlap = True
         if self.W > 1:
             for m in self.flat_owners:  # DDP's initial parameter broadcast
                 dist.broadcast(m._flat, 0)
             for m in self.hooked:
                 m.grad_hook = (self.bucket_bytes, self._make_hook(m))
+
+    def set_overlap(self, flag):
+        """In-backward bucket all-reduces on (default) or off.  Off when a step runs the
+        same model's backward more than once (ExtraTrainer's num_pred_step > 1 rollout):
+        a later backward accumulates into the flat gradient (beta = 1), so reducing after
+        the first one would race its in-flight buckets and count the earlier gradient W
+        times; the flat gradient is then reduced once in finish()."""
+        flag = bool(flag)
+        if flag == self.overlap:
+            return
+        self.overlap = flag
+        if self.W > 1:
+            for m in self.hooked:
+                m.grad_hook = (self.bucket_bytes, self._make_hook(m)) if flag else None
 
     def _make_hook(self, owner):
         def hook(lo, hi):
@@ -71,7 +86,7 @@ class GradSync:
         """Wait for the bucket all-reduces and apply the 1/W factor (HIP kernel)."""
         if self.W == 1:
             return
-        for m in self.post:
+        for m in (self.post if self.overlap else self.flat_owners):
             if m._flat_grad is not None and any(p.grad is not None for p in m.parameters()):
                 self.works.append(dist.all_reduce(m._flat_grad, op=dist.ReduceOp.SUM, async_op=True))
         self.wait()

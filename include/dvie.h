@@ -61,6 +61,9 @@ extern "C" {
  *   y = v.
  * Constraints: c % (16/sizeof(elem)) == 0, cout % 4 == 0, every ld % 4 == 0, pointers
  * 16-byte aligned for x/w and 8-byte aligned (bf16) / 16-byte (f32) for y/res/z.
+ * Size: one input image and the packed weights must each stay below 4 GiB; a larger
+ * batch runs internally as batch chunks whose input span fits (the kernels use 32-bit
+ * buffer offsets), so e.g. 448-channel bf16 activations at 1024x2048 work at any n.
  */
 typedef struct dvie_conv_desc {
   const void* x;

@@ -27,3 +27,16 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _test_local_env():
+    """Environment knobs a test (or a helper it calls) sets -- DVIE_PRECISION, the
+    DVIE_* kernel overrides -- are restored after it, so no test inherits another's
+    precision or kernel choice whatever the order they run in."""
+    saved = {k: v for k, v in os.environ.items() if k.startswith("DVIE_")}
+    yield
+    for k in [k for k in os.environ if k.startswith("DVIE_")]:
+        if k not in saved:
+            del os.environ[k]
+    os.environ.update(saved)

@@ -77,3 +77,23 @@ def test_device_loader_rank_shards_partition_epoch():
             assert shards[r] == list(perm[r::3][:3][:2])
         flat = [i for s in shards for i in s]
         assert len(set(flat)) == len(flat)
+
+
+def test_device_loader_val_covers_every_clip():
+    """Validation loader (shuffle=False) = the reference's val DistributedSampler
+    (InterTrainer.py:97-100): every clip is seen, the shard is padded to a multiple of W by
+    wrapping, and the last partial batch is kept (drop_last=False)."""
+    from torch.utils.data.distributed import DistributedSampler
+    from deep_video_interpolation_extrapolation_amd.data import DeviceClipLoader, DeviceClips
+    dc = DeviceClips.__new__(DeviceClips)
+    dc.n = 11
+    dc.batch = lambda idx: {"idx": list(int(i) for i in idx)}
+    seen = []
+    for r in range(3):
+        ld = DeviceClipLoader(dc, 3, rank=r, world=3, shuffle=False)
+        got = [b["idx"] for b in ld]
+        assert len(got) == len(ld) == 2 and [len(b) for b in got] == [3, 1]
+        flat = [i for b in got for i in b]
+        assert flat == list(DistributedSampler(range(11), num_replicas=3, rank=r))
+        seen += flat
+    assert sorted(set(seen)) == list(range(11)) and len(seen) == 12

@@ -70,7 +70,7 @@ def test_frames_only_and_epoch(dev):
 
 def test_device_loader_shards_and_epochs(dev):
     """DeviceClipLoader: rank shards of one epoch partition the store, set_epoch reshuffles,
-    and the unshuffled (val) order is the rank-strided identity."""
+    and the unshuffled (val) order is the reference val sampler's (DistributedSampler defaults)."""
     from deep_video_interpolation_extrapolation_amd.data import DeviceClipLoader, DeviceClips
     imgs, segs = _store(8, 3, 20, 36, 5)
     dc = DeviceClips(torch.from_numpy(imgs), torch.from_numpy(segs), split="val", device=dev)
@@ -89,8 +89,10 @@ def test_device_loader_shards_and_epochs(dev):
         ld.set_epoch(ep)
         got = [firsts[key(b["frame1"][i])] for b in ld for i in range(2)]
         assert got == list(np.random.RandomState(3 + ep).permutation(8)[0::2])
+    from torch.utils.data.distributed import DistributedSampler
     ld = DeviceClipLoader(dc, 2, rank=1, world=2, shuffle=False)
-    assert [firsts[key(b["frame1"][i])] for b in ld for i in range(2)] == [1, 3, 5, 7]
+    want = list(DistributedSampler(range(8), num_replicas=2, rank=1))  # the reference val sampler
+    assert [firsts[key(b["frame1"][i])] for b in ld for i in range(b["frame1"].shape[0])] == want
 
 
 def test_main_launcher_clip_store(dev, tmp_path):
