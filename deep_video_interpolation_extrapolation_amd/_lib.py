@@ -18,7 +18,7 @@ DVIE_EINVAL = 1001
 F32, BF16 = 0, 1
 ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3, 4
 EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW, EW_MASK, EW_IM2COL = range(10)
-LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC = range(6)
+LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC, LOSS_COSNHWC, LOSS_IOU, LOSS_ARGMAX_IOU = range(9)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
 OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD = 8, 9, 10, 11
 

@@ -1,13 +1,15 @@
 // Loss / metric reductions (fp32 math, double cross-block accumulation, deterministic):
 // L1, gradient-difference (GDL), SSIM (11x11 gaussian, separable, LDS-tiled), per-sample
-// MSE (PSNR), softmax cross-entropy against argmax(one-hot), and the VGG feature L1.
+// MSE (PSNR), softmax cross-entropy against argmax(one-hot), the VGG feature L1, and the
+// validation metrics VGG feature cosine and IoU (pixel accuracy).
 // Each kernel writes per-block partial sums; a one-block kernel folds them into the
 // output scalar(s).  When a gradient buffer is given, the kernels also write
 // d(weight*loss)/d(pred) in NCHW-contiguous fp32 (the autograd wrappers scale it by
 // the incoming gradient).
 //
 // Reference: losses.py:18-48 (_ssim / create_window), 63-87 (SSIM), 103-116 (PSNR),
-// 137-151 (GDLLoss), 157-180 (VGGLoss feature L1), nn.L1Loss (losses.py:224) and
+// 122-131 (IoU), 137-151 (GDLLoss), 157-180 (VGGLoss feature L1), 182-207 (VGGCosineLoss),
+// nn.L1Loss (losses.py:224) and
 // nn.CrossEntropyLoss (runners/InterTrainer.py:75,414).
 #include "common.h"
 
@@ -167,6 +169,97 @@ __global__ __launch_bounds__(RB) void l1nhwc_kernel(const dvie_loss_desc p) {
       bv = b[sb.at(n, c, y, x)];
     }
     acc += fabsf(av - bv);
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) p.partial[blockIdx.x] = t;
+}
+
+// mean over pixels of cos(a_pix, b_pix) over the channel axis (VGGCosineLoss,
+// losses.py:182-207: a / sqrt(sum_c a^2) . b / sqrt(sum_c b^2), summed over channels).
+// A group of L lanes (a power of two) owns one pixel and strides over its channels, so a
+// wave reads 64/L neighbouring pixels' channel runs; the L partial sums meet by xor
+// shuffles.  dot / (sqrt(saa) * sqrt(sbb)) is NaN for an all-zero feature vector, as the
+// reference's 0/0 is.
+template <typename T>
+__global__ __launch_bounds__(RB) void cosnhwc_kernel(const dvie_loss_desc p, int L) {
+  __shared__ double sh[RB / 64];
+  const T* a = (const T*)p.a;
+  const T* b = (const T*)p.b;
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const long long npx = (long long)p.bsz * p.h * p.w;
+  const int lane = threadIdx.x & 63, sub = lane & (L - 1);
+  const long long groups_per_block = RB / L;
+  const long long g0 = (long long)blockIdx.x * groups_per_block + threadIdx.x / L;
+  const long long gstride = (long long)gridDim.x * groups_per_block;
+  double acc = 0.0;
+  for (long long pix = g0; pix - threadIdx.x / L < npx; pix += gstride) {  // uniform trip count per wave
+    float dot = 0.f, saa = 0.f, sbb = 0.f;
+    const bool live = pix < npx;
+    if (live) {
+      const int x = (int)(pix % p.w);
+      const int y = (int)((pix / p.w) % p.h);
+      const int n = (int)(pix / ((long long)p.w * p.h));
+      for (int c = sub; c < p.ch; c += L) {
+        float av, bv;
+        if constexpr (sizeof(T) == 2) {
+          av = bf2f(a[sa.at(n, c, y, x)]);
+          bv = bf2f(b[sb.at(n, c, y, x)]);
+        } else {
+          av = a[sa.at(n, c, y, x)];
+          bv = b[sb.at(n, c, y, x)];
+        }
+        dot += av * bv;
+        saa += av * av;
+        sbb += bv * bv;
+      }
+    }
+    for (int o = 1; o < L; o <<= 1) {
+      dot += __shfl_xor(dot, o, 64);
+      saa += __shfl_xor(saa, o, 64);
+      sbb += __shfl_xor(sbb, o, 64);
+    }
+    if (live && sub == 0) acc += (double)(dot / (sqrtf(saa) * sqrtf(sbb)));
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) p.partial[blockIdx.x] = t;
+}
+
+// pixel accuracy of two label maps (IoU, losses.py:122-131: sum(pred == gt) / (B*H*W)).
+// DVIE_LOSS_IOU: a, b are int64 (B, H, W) maps (strides sn, sh, sw; sc unused).
+// DVIE_LOSS_ARGMAX_IOU: a, b are fp32 (B, C, H, W) scores; each pixel's label is its
+// first maximal channel (torch.argmax), as validate's IoU(argmax(seg), argmax(gt_seg)).
+__global__ __launch_bounds__(RB) void iou_kernel(const dvie_loss_desc p) {
+  __shared__ double sh[RB / 64];
+  const Shape sa{p.a_sn, p.a_sc, p.a_sh, p.a_sw}, sb{p.b_sn, p.b_sc, p.b_sh, p.b_sw};
+  const long long npx = (long long)p.bsz * p.h * p.w;
+  double acc = 0.0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < npx;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(e % p.w);
+    const int y = (int)((e / p.w) % p.h);
+    const int n = (int)(e / ((long long)p.w * p.h));
+    long long la, lb;
+    if (p.kind == DVIE_LOSS_IOU) {
+      la = ((const long long*)p.a)[sa.at(n, 0, y, x)];
+      lb = ((const long long*)p.b)[sb.at(n, 0, y, x)];
+    } else {
+      const float* a = (const float*)p.a;
+      const float* b = (const float*)p.b;
+      float ba = a[sa.at(n, 0, y, x)], bb = b[sb.at(n, 0, y, x)];
+      la = lb = 0;
+      for (int c = 1; c < p.ch; ++c) {
+        const float ta = a[sa.at(n, c, y, x)], tb = b[sb.at(n, c, y, x)];
+        if (ta > ba || (ta != ta && ba == ba)) {  // torch.argmax: NaN is the maximum
+          ba = ta;
+          la = c;
+        }
+        if (tb > bb || (tb != tb && bb == bb)) {
+          bb = tb;
+          lb = c;
+        }
+      }
+    }
+    acc += la == lb ? 1.0 : 0.0;
   }
   const double t = block_sum(acc, sh);
   if (threadIdx.x == 0) p.partial[blockIdx.x] = t;
@@ -346,6 +439,14 @@ struct LossPlan {
   dim3 grid;
 };
 
+// lanes per pixel of the cosine kernel: the channel count rounded up to a power of two,
+// capped at one wave
+static int cos_lanes(int ch) {
+  int L = 1;
+  while (L < ch && L < 64) L <<= 1;
+  return L;
+}
+
 static LossPlan plan_loss(const dvie_loss_desc& d) {
   LossPlan lp{};
   const long long px = (long long)d.bsz * d.h * d.w;
@@ -365,6 +466,14 @@ static LossPlan plan_loss(const dvie_loss_desc& d) {
       lp.grid = dim3(lp.blocks);
       break;
     }
+    case DVIE_LOSS_COSNHWC: {
+      long long b = (px * cos_lanes(d.ch) + RB * 8 - 1) / (RB * 8);
+      lp.blocks = (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
+      lp.grid = dim3(lp.blocks);
+      break;
+    }
+    case DVIE_LOSS_IOU:
+    case DVIE_LOSS_ARGMAX_IOU:
     case DVIE_LOSS_CE: {
       long long b = (px + RB * 4 - 1) / (RB * 4);
       lp.blocks = (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
@@ -399,6 +508,8 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
   DVIE_CHECK_ARG(d->bsz > 0 && d->ch > 0 && d->h > 0 && d->w > 0, "loss: empty shape");
   if (d->kind == DVIE_LOSS_GDL) DVIE_CHECK_ARG(d->h > 1 && d->w > 1, "loss: GDL needs h,w > 1");
   if (d->kind == DVIE_LOSS_SSIM && d->grad) DVIE_CHECK_ARG(d->ws != nullptr, "loss: SSIM grad needs ws");
+  if (d->kind >= DVIE_LOSS_COSNHWC)
+    DVIE_CHECK_ARG(d->grad == nullptr, "loss: kind %d is a metric (no gradient)", d->kind);
   hipStream_t s = (hipStream_t)stream;
   const LossPlan lp = plan_loss(*d);
   const double px = (double)d->bsz * d->h * d->w;
@@ -431,6 +542,19 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
       else
         hipLaunchKernelGGL(l1nhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d);
       hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / tot, 0.0);
+      break;
+    case DVIE_LOSS_COSNHWC:
+      if (d->dtype == DVIE_BF16)
+        hipLaunchKernelGGL(cosnhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
+      else
+        hipLaunchKernelGGL(cosnhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
+                         (double)d->weight / px, 0.0);
+      break;
+    case DVIE_LOSS_IOU:
+    case DVIE_LOSS_ARGMAX_IOU:
+      hipLaunchKernelGGL(iou_kernel, lp.grid, dim3(RB), 0, s, *d);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0);
       break;
     default:
       DVIE_CHECK_ARG(false, "loss: unknown kind %d", d->kind);

@@ -132,11 +132,43 @@ class PSNR(nn.Module):
             return (10 * torch.log10(self.max_level * self.max_level / mse)).mean()
 
 
+def _metric(kind, a, b, ch, dtype=None, strides=None, weight=1.0):
+    """One metric reduction (dvie_loss kinds COSNHWC / IOU / ARGMAX_IOU) -> 0-dim fp32."""
+    L.require_gpu(a)
+    lib = L.load()
+    d = L.LossDesc()
+    d.kind, d.a, d.b = kind, a.data_ptr(), b.data_ptr()
+    sa, sb = strides if strides is not None else (a.stride(), b.stride())
+    d.a_sn, d.a_sc, d.a_sh, d.a_sw = sa
+    d.b_sn, d.b_sc, d.b_sh, d.b_sw = sb
+    d.bsz, d.ch, d.h, d.w = a.shape[0], ch, a.shape[-2], a.shape[-1]
+    d.weight = weight
+    d.dtype = L.F32 if dtype is None else dtype
+    part = torch.empty(max(1, lib.dvie_loss_partial_count(ctypes.byref(d))), dtype=torch.float64, device=a.device)
+    out = torch.empty(1, dtype=torch.float32, device=a.device)
+    d.partial, d.out = part.data_ptr(), out.data_ptr()
+    L.check(lib.dvie_loss(ctypes.byref(d), L.stream_ptr(a.device)), f"metric kind {kind}")
+    return out[0]
+
+
 class IoU(nn.Module):
+    """Reference losses.py:122-131: fraction of pixels whose labels agree (a pixel
+    accuracy, named IoU there).  pred / gt: (B, H, W) integer label maps."""
+
     def forward(self, pred, gt):
         assert pred.size() == gt.size()
-        bs, h, w = gt.size()
-        return (pred == gt).float().sum() / (bs * h * w)
+        assert pred.dim() == 3
+        a, b = pred.long(), gt.long()
+        return _metric(L.LOSS_IOU, a, b, 1,
+                       strides=((a.stride(0), 0, a.stride(1), a.stride(2)), (b.stride(0), 0, b.stride(1), b.stride(2))))
+
+    @staticmethod
+    def of_scores(pred_scores, gt_scores):
+        """IoU(argmax(pred_scores, 1), argmax(gt_scores, 1)) with both argmaxes fused into
+        the reduction (validate, runners/InterTrainer.py:615-624)."""
+        assert pred_scores.shape == gt_scores.shape and pred_scores.dim() == 4
+        a, b = _f32(pred_scores), _f32(gt_scores)
+        return _metric(L.LOSS_ARGMAX_IOU, a, b, a.shape[1])
 
 
 class VGGLoss(nn.Module):
@@ -158,15 +190,22 @@ class VGGCosineLoss(nn.Module):
         self.vgg_net = my_vgg(vgg19_features(weights))
 
     def forward(self, input, gt, normed=True):
+        """One VGG plan over [input | gt] (2B images), then per feature level one HIP
+        reduction of the per-pixel channel cosine between the two halves (NHWC, in the
+        plan's compute dtype); the mean over the 5 levels is the score."""
+        assert input.shape == gt.shape
+        n = input.shape[0]
         with torch.no_grad():
-            fi = [f.float().clone() for f in self.vgg_net.features_nhwc(input, normalize=not normed)]
-            fg = [f.float() for f in self.vgg_net.features_nhwc(gt, normalize=not normed)]
-            score = 0
-            for a, b in zip(fi, fg):
-                a = a / torch.sqrt(torch.sum(a ** 2, dim=-1, keepdim=True))
-                b = b / torch.sqrt(torch.sum(b ** 2, dim=-1, keepdim=True))
-                score += torch.mean(torch.sum(a * b, dim=-1))
-            return score / len(fi)
+            feats = self.vgg_net.features_nhwc(torch.cat([_f32(input), _f32(gt)], 0), normalize=not normed)
+            dt = L.BF16 if feats[0].dtype == torch.bfloat16 else L.F32
+            scores = []
+            for f in feats:
+                a, b = f[:n], f[n:]
+                sn, sh, sw, sc = a.stride()
+                st = (sn, sc, sh, sw)
+                scores.append(_metric(L.LOSS_COSNHWC, a.permute(0, 3, 1, 2), b.permute(0, 3, 1, 2), f.shape[-1],
+                                      dtype=dt, strides=(st, st), weight=1.0 / len(feats)))
+            return torch.stack(scores).sum()
 
 
 class RGBLoss(nn.Module):

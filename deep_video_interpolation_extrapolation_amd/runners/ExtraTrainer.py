@@ -133,8 +133,8 @@ class ExtraTrainer(InterTrainer):
                         d[p + "coarse_l1"] = self.L1Loss(im, gt)
                         d[p + "coarse_psnr"] = self.PSNRLoss(im, gt)
                         d[p + "coarse_ssim"] = 1 - self.SSIMLoss(im, gt)
-                        d[p + "coarse_iou"] = self.IoULoss(torch.argmax(coarse_seg[:, 20 * j:20 * j + 20], dim=1),
-                                                           torch.argmax(gt_seg[:, 20 * j:20 * j + 20], dim=1))
+                        d[p + "coarse_iou"] = self.IoULoss.of_scores(coarse_seg[:, 20 * j:20 * j + 20],
+                                                                     gt_seg[:, 20 * j:20 * j + 20])
                         d[p + "coarse_vgg"] = self.VGGCosLoss(im, gt, False)
                     if nps == 1:
                         break

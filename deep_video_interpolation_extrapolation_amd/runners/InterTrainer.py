@@ -86,9 +86,11 @@ class InterTrainer:
                 self.val_loader = torch.utils.data.DataLoader(
                     self.val_set, batch_size=max(1, args.batch_size // args.gpus), shuffle=False,
                     num_workers=getattr(args, "num_workers", 0), pin_memory=True, sampler=sampler)
-        # (a subclass that builds more optimizers loads after them: _defer_load)
-        if not getattr(self, "_defer_load", False) and (getattr(args, "resume", False)
-                                                        or getattr(args, "load_coarse", False)):
+        # reference l.105-106 (a subclass that builds more optimizers loads after them:
+        # _defer_load)
+        if not getattr(self, "_defer_load", False) and (
+                getattr(args, "resume", False) or (args.split != "train" and not getattr(args, "checkepoch_range", False))
+                or getattr(args, "load_coarse", False) or getattr(args, "load_refine", False)):
             self.load_checkpoint()
 
     def _device_loader(self, split, shuffle):
@@ -188,7 +190,7 @@ class InterTrainer:
                 d["coarse_psnr"] = self.PSNRLoss(a, b)
                 d["coarse_ssim"] = 1 - self.SSIMLoss(a, b)
                 if self.args.mode == "xs2xs":
-                    d["coarse_iou"] = self.IoULoss(torch.argmax(coarse_seg, dim=1), torch.argmax(gt_seg, dim=1))
+                    d["coarse_iou"] = self.IoULoss.of_scores(coarse_seg, gt_seg)  # IoU(argmax, argmax), fused
                 d["coarse_vgg"] = self.VGGCosLoss(a, b, False)
                 d = comm.sync_losses(d, self.W)
                 if self.rank == 0:
@@ -226,11 +228,12 @@ class InterTrainer:
         name = self._ckpt_name(a.load_model, a.checksession, a.checkepoch, a.checkpoint, a.load_dir or ".")
         self.log.info("Loading checkpoint %s" % name)
         ckpt = torch.load(name, map_location="cpu", weights_only=True)
-        if getattr(a, "load_coarse", False) or getattr(a, "resume", False):
+        # weights gated by load_coarse, optimizer state by train_coarse and load_coarse (l.902-936)
+        if getattr(a, "load_coarse", False):
             sd = self.model.module.coarse_model.state_dict()
             sd.update(ckpt["coarse_model"])
             self.model.module.coarse_model.load_state_dict(sd)
-        if a.split == "train" and getattr(a, "train_coarse", False) and "coarse_opt" in ckpt:
+        if a.split == "train" and getattr(a, "train_coarse", False) and getattr(a, "load_coarse", False):
             self.coarse_opt.load_state_dict(ckpt["coarse_opt"])
         # epoch bookkeeping as the reference (l.953-958): the file's epoch is checkepoch + 1
         if getattr(a, "resume", False):

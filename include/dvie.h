@@ -251,6 +251,17 @@ int dvie_ew(const dvie_ew_desc* d, void* stream);
 #define DVIE_LOSS_MSE 3
 #define DVIE_LOSS_CE 4
 #define DVIE_LOSS_L1NHWC 5 /* mean|a-b| over NHWC tensors of elem type dtype (VGG features) */
+/* validation metrics (no gradient; `grad` must be NULL):
+ *  COSNHWC    : weight * mean_pix( sum_c a.b / (|a| |b|) ) over (B, C=ch, H, W) tensors of
+ *               elem type dtype, channel stride a_sc/b_sc (VGGCosineLoss, losses.py:182-207;
+ *               NaN for an all-zero feature vector, as the reference's 0/0)
+ *  IOU        : mean_pix( a == b ) of int64 label maps (B, H, W), strides a_sn/a_sh/a_sw
+ *               (IoU, losses.py:122-131)
+ *  ARGMAX_IOU : IOU of argmax_c a and argmax_c b, fp32 (B, C, H, W) scores (first maximum,
+ *               as torch.argmax; InterTrainer.validate, runners/InterTrainer.py:615-624) */
+#define DVIE_LOSS_COSNHWC 6
+#define DVIE_LOSS_IOU 7
+#define DVIE_LOSS_ARGMAX_IOU 8
 
 typedef struct dvie_loss_desc {
   const void* a;

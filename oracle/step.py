@@ -45,7 +45,7 @@ def inter_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(8
     (loss / world).backward()
     grads = {k: v.grad.detach().clone() for k, v in P.items()}
     new, state = adamax(params, grads, lr, state)
-    return OrderedDict((k, float(v)) for k, v in ld.items()), grads, new, state, (rgb.detach(), seg_out.detach())
+    return OrderedDict((k, float(v.detach())) for k, v in ld.items()), grads, new, state, (rgb.detach(), seg_out.detach())
 
 
 def adamax(params, grads, lr, state=None, betas=(0.9, 0.999), eps=1e-8):

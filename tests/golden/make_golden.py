@@ -23,6 +23,8 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
                      logvar, parameter-gradient stats, initial-weight checksums, running stats
   step.npz       G4: one training step of the reference modules (InterTrainer.py:380-441
                      body): loss dict, per-parameter gradient stats, post-Adamax checksums
+  ckpt_manifest.json G10: the reference save_checkpoint dict (InterTrainer.py:867-885)
+                     after the G4 step, written by torch.save and read back: its manifest
 """
 import os
 import sys
@@ -280,9 +282,61 @@ def g9():
     np.savez_compressed(os.path.join(HERE, "vaehrnet.npz"), **out)
 
 
+def _tstat(t):
+    t = t.detach()
+    return {"dtype": str(t.dtype).replace("torch.", ""), "shape": list(t.shape),
+            "sum": float(t.double().sum()), "sumsq": float((t.double() ** 2).sum())}
+
+
+def g10():
+    """Checkpoint format (reference runners/InterTrainer.py:867-885 save_checkpoint): the
+    reference modules take the G4 training step, then the reference's save_dict is written
+    with torch.save and read back.  The file itself is ~120 MB (9.9 M fp32 weights + two
+    Adamax state tensors each), so the fixture is its manifest: top-level keys and values,
+    every state_dict entry in order with dtype / shape / sum / sum of squares, and the
+    optimizer state_dict's param_groups and per-index state the same way.  Tests rebuild
+    the file from the oracle step (pinned by G4) and check it against this manifest before
+    loading it."""
+    import json
+    import tempfile
+    args = args_ns()
+    torch.manual_seed(1024)
+    model = ref_nets.InterNet(args)
+    rgb_loss = ref_losses.RGBLoss(args)
+    ce = torch.nn.CrossEntropyLoss()
+    coarse_opt = torch.optim.Adamax(list(model.coarse_model.parameters()), lr=1e-3)
+    data = inputs.step_batch(2, 32, 64)
+    x = torch.cat([data["frame1"], data["frame3"]], dim=1)
+    seg = torch.cat([data["seg1"], data["seg3"]], dim=1)
+    coarse_img, coarse_seg = model(x, seg=seg)
+    ld = rgb_loss(coarse_img, data["frame2"], False, prefix="coarse")
+    ld["coarse_ce_loss"] = args.ce_weight * ce(coarse_seg, torch.argmax(data["seg2"], dim=1))
+    loss = 0
+    for v in ld.values():
+        loss += torch.mean(v)
+    coarse_opt.zero_grad()
+    loss.backward()
+    coarse_opt.step()
+    # save_checkpoint (session 1, epoch 1 -> 'epoch': 2, step 0)
+    save_dict = {"session": 1, "epoch": 1 + 1, "coarse_model": model.coarse_model.state_dict(),
+                 "coarse_opt": coarse_opt.state_dict()}
+    name = "{}_{}_{}_{}".format("InterNet", "xs2xs", "inter", 1) + "_{}_{}.pth".format(1, 0)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, name)
+        torch.save(save_dict, path)
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+    man = {"file": name, "top_keys": list(ck.keys()), "session": ck["session"], "epoch": ck["epoch"],
+           "coarse_model": [[k, _tstat(v)] for k, v in ck["coarse_model"].items()],
+           "coarse_opt": {"param_groups": [{k: v for k, v in g.items()} for g in ck["coarse_opt"]["param_groups"]],
+                          "state": {str(i): {k: (_tstat(v) if torch.is_tensor(v) else v) for k, v in st.items()}
+                                    for i, st in ck["coarse_opt"]["state"].items()}}}
+    with open(os.path.join(HERE, "ckpt_manifest.json"), "w") as f:
+        json.dump(man, f, indent=0, sort_keys=False)
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()
