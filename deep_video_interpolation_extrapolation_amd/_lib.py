@@ -20,7 +20,9 @@ ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3, 4
 EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW, EW_MASK, EW_IM2COL = range(10)
 LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC, LOSS_COSNHWC, LOSS_IOU, LOSS_ARGMAX_IOU = range(9)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
-OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD = 8, 9, 10, 11
+OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD, OP_ATTN = 8, 9, 10, 11, 12
+(ATTN_L2NORM, ATTN_L2NORM_BWD, ATTN_CORR, ATTN_GATHER, ATTN_GATHER_T, ATTN_SOFTMAX, ATTN_SOFTMAX_BWD, ATTN_WNORM,
+ ATTN_WNORM_BWD, ATTN_POOL, ATTN_POOL_T) = range(11)
 
 vp = ctypes.c_void_p
 i32 = ctypes.c_int
@@ -159,6 +161,18 @@ class SnLayer(ctypes.Structure):
     ]
 
 
+class AttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("a", vp), ("b0", vp), ("b1", vp), ("y", vp), ("res", vp), ("z", vp),
+        ("a_ld", i64), ("b_ld", i64), ("y_ld", i64), ("res_ld", i64), ("z_ld", i64),
+        ("op", i32), ("n", i32), ("h", i32), ("w", i32),
+        ("c", i32), ("wh", i32), ("ww", i32), ("nhalf", i32),
+        ("half0", i32), ("act", i32), ("dact", i32), ("beta", i32),
+        ("dtype", i32), ("pad0", i32),
+        ("alpha", f32), ("pad1", f32),
+    ]
+
+
 class PackList(ctypes.Structure):
     _fields_ = [("descs_dev", vp), ("n", i32), ("max_elems", i32)]
 
@@ -167,6 +181,7 @@ class _OpUnion(ctypes.Union):
     _fields_ = [
         ("conv", ConvDesc), ("wgrad", WgradDesc), ("wreduce", WreduceDesc), ("colsum", ColsumDesc),
         ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList), ("bn", BnDesc), ("head", HeadDesc),
+        ("attn", AttnDesc),
     ]
 
 
@@ -176,7 +191,7 @@ class Op(ctypes.Structure):
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
-        100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
+        OP_ATTN: AttnDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
 
 EXPORTS = [
     "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
@@ -184,7 +199,7 @@ EXPORTS = [
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
-    "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep",
+    "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn",
 ]
 
 _lib = None
@@ -218,7 +233,7 @@ def load():
         lib.dvie_last_error.restype = ctypes.c_char_p
         for name in ("dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_ew",
                      "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_head_fwd",
-                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_clip_prep"):
+                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_clip_prep", "dvie_attn"):
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]

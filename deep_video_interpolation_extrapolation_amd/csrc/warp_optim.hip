@@ -379,6 +379,7 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
       case DVIE_OP_BN_BWD: rc = dvie_bn_bwd(&o.u.bn, stream); break;
       case DVIE_OP_HEAD_FWD: rc = dvie_head_fwd(&o.u.head, stream); break;
       case DVIE_OP_HEAD_BWD: rc = dvie_head_bwd(&o.u.head, stream); break;
+      case DVIE_OP_ATTN: rc = dvie_attn(&o.u.attn, stream); break;
       default: set_error("run_ops: unknown op kind %d at %d", o.kind, i); return DVIE_EINVAL;
     }
     if (rc != DVIE_OK) {
@@ -406,6 +407,7 @@ size_t dvie_abi_sizeof(int which) {
     case DVIE_OP_PACK: return sizeof(dvie_pack_desc);
     case DVIE_OP_BN_FWD: return sizeof(dvie_bn_desc);
     case DVIE_OP_HEAD_FWD: return sizeof(dvie_head_desc);
+    case DVIE_OP_ATTN: return sizeof(dvie_attn_desc);
     case 100: return sizeof(dvie_warp_desc);
     case 101: return sizeof(dvie_softmax_desc);
     case 102: return sizeof(dvie_sn_layer);

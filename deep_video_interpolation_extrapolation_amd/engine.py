@@ -108,7 +108,11 @@ class ConvLayer:
         self.stride = module.stride[0]
         self.pad = module.padding[0]
         assert module.stride[0] == module.stride[1] and module.padding[0] == module.padding[1]
-        assert module.dilation == (1, 1) and module.groups == 1
+        dil = tuple(getattr(module, "dilation", (1, 1)))
+        assert dil[0] == dil[1] and module.groups == 1
+        self.dil = dil[0]  # atrous convs (nets/refine_nets.py:60-69,210-219): taps dil apart
+        assert self.dil == 1 or (self.stride == 1 and not isinstance(module, torch.nn.ConvTranspose2d)), \
+            "dilation > 1 needs stride 1"
         self.has_bias = module.bias is not None
         self.trainable = trainable
         self.cmap = None  # packed input position -> source input channel (or -1)
@@ -129,11 +133,16 @@ class ConvLayer:
             assert self.cin_p == cin_p and self.cmap == list(cmap), f"{self.name}: inconsistent input packing"
 
     def fwd_taps(self):
-        return dict(th=self.kh, tw=self.kw, dy0=-self.pad, dx0=-self.pad, ddy=1, ddx=1, kh0=0, kw0=0, dkh=1, dkw=1)
+        d = self.dil
+        return dict(th=self.kh, tw=self.kw, dy0=-self.pad, dx0=-self.pad, ddy=d, ddx=d, kh0=0, kw0=0, dkh=1, dkw=1)
 
     def dgrad_phases(self, H, W):
         """Stride-s data gradient as s*s stride-1 convs over the output gradient."""
         s, p = self.stride, self.pad
+        if s == 1:  # one phase; taps by increasing input offset p - k*dil, k = kh-1 .. 0
+            d = self.dil
+            return [dict(ry=0, rx=0, oh=H, ow=W, th=self.kh, tw=self.kw, kh0=self.kh - 1, kw0=self.kw - 1,
+                         dkh=-1, dkw=-1, dy0=p - (self.kh - 1) * d, dx0=p - (self.kw - 1) * d, ddy=d, ddx=d)]
         phases = []
         for ry in range(s):
             khs = [k for k in range(self.kh) if (ry + p - k) % s == 0]
@@ -195,11 +204,28 @@ class LinearAsConv:
 
 
 class FuseOp(_Op):
-    def __init__(self, srcs, out, act, align=False):
-        self.srcs, self.out, self.act, self.align = srcs, out, act, align
+    """out = act(sum of the srcs, each bilinearly resized to out's grid).  detach: no
+    gradient flows back to the srcs (the reference's .detach() before an interpolate,
+    e.g. nets/refine_nets.py:111)."""
+
+    def __init__(self, srcs, out, act, align=False, detach=False):
+        self.srcs, self.out, self.act, self.align, self.detach = srcs, out, act, align, detach
 
     def inputs(self):
         return list(self.srcs)
+
+
+class AttnOp(_Op):
+    """One dvie_attn op (kind: l2norm / corr / softmax / wnorm / gather / pool) reading `a`
+    and the target maps `bs`, writing `out`; c = the channels it reduces or writes."""
+
+    def __init__(self, kind, a, bs, out, c, wh=1, ww=1, nhalf=1, half0=0):
+        self.kind, self.a, self.bs, self.out, self.c = kind, a, list(bs), out, c
+        self.wh, self.ww, self.nhalf, self.half0 = wh, ww, nhalf, half0
+        self.act = L.ACT_NONE
+
+    def inputs(self):
+        return [self.a] + self.bs
 
 
 class PoolOp(_Op):
@@ -312,8 +338,8 @@ class Graph:
         lay = self.layer(module, trainable, name)
         lay.bind_input(x.c, cmap)
         assert out.c == lay.cout_p, (name, out.c, lay.cout_p)
-        oh = (x.H + 2 * lay.pad - lay.kh) // lay.stride + 1
-        ow = (x.W + 2 * lay.pad - lay.kw) // lay.stride + 1
+        oh = (x.H + 2 * lay.pad - lay.dil * (lay.kh - 1) - 1) // lay.stride + 1
+        ow = (x.W + 2 * lay.pad - lay.dil * (lay.kw - 1) - 1) // lay.stride + 1
         assert (out.H, out.W) == (oh, ow), (name, out.H, out.W, oh, ow)
         if res is not None:
             assert (res.H, res.W, res.c) == (out.H, out.W, out.c)
@@ -333,11 +359,47 @@ class Graph:
         self._add(ConvTOp(x, lay, out, act))
         return out
 
-    def fuse(self, srcs, out, act=L.ACT_NONE, align=False):
+    def fuse(self, srcs, out, act=L.ACT_NONE, align=False, detach=False):
         assert 1 <= len(srcs) <= 3
         for s in srcs:
             assert s.c == out.c
-        self._add(FuseOp(srcs, out, act, align))
+        self._add(FuseOp(srcs, out, act, align, detach))
+        return out
+
+    # ---- local-window attention (dvie_attn; MSResAttnRefine, nets/refine_nets.py:253-323) ----
+    def l2norm(self, x, out):
+        """out = x / |x| over the channels of each pixel."""
+        assert (x.H, x.W, x.c) == (out.H, out.W, out.c)
+        self._add(AttnOp("l2norm", x, [], out, x.c))
+        return out
+
+    def corr(self, x, targets, out, wh, ww):
+        """out[p, m*K + k] = <x(p), targets[m](p + o_k)> (K = wh*ww window entries)."""
+        K = wh * ww
+        assert out.c >= len(targets) * K and all(t.c == x.c and (t.H, t.W) == (x.H, x.W) for t in targets)
+        self._add(AttnOp("corr", x, list(targets), out, x.c, wh=wh, ww=ww, nhalf=len(targets)))
+        return out
+
+    def softmax(self, x, out, nhalf, wh, ww):
+        """softmax over the first nhalf*wh*ww channels of each pixel."""
+        self._add(AttnOp("softmax", x, [], out, x.c, wh=wh, ww=ww, nhalf=nhalf))
+        return out
+
+    def wnorm(self, x, out, nhalf, wh, ww):
+        """per map m: out[:, m*K:(m+1)*K] = x / sum over those K channels."""
+        self._add(AttnOp("wnorm", x, [], out, x.c, wh=wh, ww=ww, nhalf=nhalf))
+        return out
+
+    def gather(self, w, feats, out, half0, nhalf, wh, ww):
+        """out(p) = sum_m sum_k w[p, (half0+m)*K + k] * feats[m](p + o_k)."""
+        assert all(f.c == out.c and (f.H, f.W) == (out.H, out.W) for f in feats) and 1 <= len(feats) <= 2
+        self._add(AttnOp("gather", w, list(feats), out, out.c, wh=wh, ww=ww, nhalf=nhalf, half0=half0))
+        return out
+
+    def apool(self, x, out, ph, pw):
+        """F.avg_pool2d(x, (ph, pw), stride 1, padding (ph//2, pw//2), count_include_pad=False)."""
+        assert (x.H, x.W, x.c) == (out.H, out.W, out.c)
+        self._add(AttnOp("pool", x, [], out, x.c, wh=ph, ww=pw))
         return out
 
     def mask(self, src, out, key, chan, inverse=False):
@@ -348,6 +410,11 @@ class Graph:
     def output_nchw(self, key, region, channels):
         self._add(OutNCHWOp(region, key, channels))
         self.outputs[key] = (region, channels)
+
+    def export_nchw(self, key, region, channels):
+        """Copy a region to an external NCHW fp32 tensor with no gradient path (a detached
+        side output, e.g. HRNet's seg-encoder features for the refinement stage)."""
+        self._add(OutNCHWOp(region, key, channels))
 
     def pool(self, x, out):
         assert (out.H * 2, out.W * 2, out.c) == (x.H, x.W, x.c)
@@ -440,6 +507,8 @@ class Plan:
                     need = op.layer.trainable or any(r.buf.needs_grad for r in op.inputs())
                 elif isinstance(op, BNOp):
                     need = op.trainable or op.x.buf.needs_grad
+                elif isinstance(op, FuseOp) and op.detach:
+                    need = False
                 else:
                     need = any(r.buf.needs_grad for r in op.inputs())
                 op.out.buf.needs_grad = op.out.buf.needs_grad or need
@@ -452,6 +521,8 @@ class Plan:
                 b.read_region = None
                 b.done = False
             for op in g.ops:
+                if isinstance(op, FuseOp) and op.detach:
+                    continue
                 for r in op.inputs():
                     if r.buf.needs_grad:
                         r.buf.expected += 1
@@ -625,6 +696,8 @@ class Plan:
                     o.meta = dict(cls="conv_fwd", name=lay.name, flops=2.0 * npx * lay.cout * lay.cin * ph["th"] * ph["tw"],
                                   bytes=float(self.es * (nf * x.H * x.W * lay.cout + npx * lay.cin)))
                     self.fwd.append(o)
+            elif isinstance(op, AttnOp):
+                self.fwd.append(self._attn_fwd(op))
             elif isinstance(op, FuseOp):
                 out = op.out
                 srcs = [(self.ptr(s), s.buf.C, s.H, s.W) for s in op.srcs]
@@ -689,6 +762,90 @@ class Plan:
                 self.fwd.append(o)
             else:
                 raise TypeError(op)
+
+    # ---------------- local-window attention ----------------
+    _ATTN_FWD = {"l2norm": L.ATTN_L2NORM, "corr": L.ATTN_CORR, "softmax": L.ATTN_SOFTMAX, "wnorm": L.ATTN_WNORM,
+                 "gather": L.ATTN_GATHER, "pool": L.ATTN_POOL}
+
+    def attn_desc(self, kind, n, region_hw, c, a, a_ld, y, y_ld, b0=None, b1=None, b_ld=0, wh=1, ww=1, nhalf=1,
+                  half0=0, res=None, res_ld=0, z=None, z_ld=0, dact=0, beta=0):
+        o = self._op(L.OP_ATTN)
+        d = o.u.attn
+        d.op, d.n, d.h, d.w, d.c = kind, n, region_hw[0], region_hw[1], c
+        d.a, d.a_ld, d.y, d.y_ld, d.b0, d.b1, d.b_ld = a, a_ld, y, y_ld, b0, b1, b_ld
+        d.wh, d.ww, d.nhalf, d.half0 = wh, ww, nhalf, half0
+        d.res, d.res_ld, d.z, d.z_ld, d.dact, d.beta = res, res_ld, z, z_ld, dact, beta
+        d.dtype, d.alpha = self.dt, 0.2
+        return o
+
+    def _attn_fwd(self, op):
+        a, out = op.a, op.out
+        bs = [self.ptr(b) for b in op.bs] + [None, None]
+        b_ld = op.bs[0].buf.C if op.bs else 0
+        if len(op.bs) == 2:
+            assert op.bs[1].buf.C == b_ld, "attn: target maps need one pixel stride"
+        o = self.attn_desc(self._ATTN_FWD[op.kind], self.nf, (out.H, out.W), op.c, self.ptr(a), a.buf.C,
+                           self.ptr(out), out.buf.C, bs[0], bs[1], b_ld, op.wh, op.ww, op.nhalf, op.half0)
+        npx = self.nf * out.H * out.W
+        o.meta = dict(cls="attn", name=f"{op.kind}:{out.buf.name}", flops=0.0,
+                      bytes=float(self.es * npx * (a.c + sum(b.c for b in op.bs) + out.c)))
+        return o
+
+    def _attn_backward(self, op, gout, gld):
+        """Gradient contributions of one attention op (formulas in include/dvie.h)."""
+        nb = self.nb
+        a, out = op.a, op.out
+        hw = (out.H, out.W)
+        K = op.wh * op.ww
+        ld_a = a.buf.C
+
+        def contrib(region, build):
+            if region.buf.needs_grad:
+                self._contrib(region, lambda beta, res, res_ld, dact, z, z_ld:
+                              [build(dict(res=res, res_ld=res_ld, dact=dact, z=z, z_ld=z_ld, beta=beta))])
+
+        if op.kind == "l2norm":  # a = x, out = x / |x|
+            contrib(a, lambda e: self.attn_desc(L.ATTN_L2NORM_BWD, nb, hw, op.c, gout, gld, self.ptr(a, grad=True),
+                                                ld_a, self.ptr(out), self.ptr(a), self._same_ld(out, a), **e))
+        elif op.kind == "softmax":
+            contrib(a, lambda e: self.attn_desc(L.ATTN_SOFTMAX_BWD, nb, hw, op.c, gout, gld, self.ptr(a, grad=True),
+                                                ld_a, self.ptr(out), None, out.buf.C, op.wh, op.ww, op.nhalf, **e))
+        elif op.kind == "wnorm":
+            contrib(a, lambda e: self.attn_desc(L.ATTN_WNORM_BWD, nb, hw, op.c, gout, gld, self.ptr(a, grad=True),
+                                                ld_a, self.ptr(out), self.ptr(a), self._same_ld(out, a), op.wh,
+                                                op.ww, op.nhalf, **e))
+        elif op.kind == "pool":
+            contrib(a, lambda e: self.attn_desc(L.ATTN_POOL_T, nb, hw, op.c, gout, gld, self.ptr(a, grad=True), ld_a,
+                                                wh=op.wh, ww=op.ww, **e))
+        elif op.kind == "corr":  # S[p, m*K+k] = <a(p), b_m(p+o_k)>
+            bs = op.bs
+            bp = [self.ptr(b) for b in bs] + [None]
+            contrib(a, lambda e: self.attn_desc(L.ATTN_GATHER, nb, hw, op.c, gout, gld, self.ptr(a, grad=True), ld_a,
+                                                bp[0], bp[1], bs[0].buf.C, op.wh, op.ww, op.nhalf, 0, **e))
+            for m, b in enumerate(bs):
+                contrib(b, lambda e, m=m, b=b: self.attn_desc(
+                    L.ATTN_GATHER_T, nb, hw, op.c, gout, gld, self.ptr(b, grad=True), b.buf.C, self.ptr(a), None,
+                    ld_a, op.wh, op.ww, op.nhalf, m, **e))
+        elif op.kind == "gather":  # out(p) = sum_m sum_k a[p, (half0+m)K + k] f_m(p + o_k)
+            fs = op.bs
+            maps = [None] * op.nhalf
+            for m, f in enumerate(fs):
+                maps[op.half0 + m] = self.ptr(f)
+            assert op.nhalf <= 2
+            maps += [None]
+            contrib(a, lambda e: self.attn_desc(L.ATTN_CORR, nb, hw, out.c, gout, gld, self.ptr(a, grad=True), ld_a,
+                                                maps[0], maps[1], fs[0].buf.C, op.wh, op.ww, op.nhalf, **e))
+            for m, f in enumerate(fs):
+                contrib(f, lambda e, m=m, f=f: self.attn_desc(
+                    L.ATTN_GATHER_T, nb, hw, out.c, self.ptr(a), ld_a, self.ptr(f, grad=True), f.buf.C, gout, None,
+                    gld, op.wh, op.ww, op.nhalf, op.half0 + m, **e))
+        else:
+            raise TypeError(op.kind)
+
+    @staticmethod
+    def _same_ld(r0, r1):
+        assert r0.buf.C == r1.buf.C, f"attn backward: {r0.buf} and {r1.buf} need one pixel stride"
+        return r0.buf.C
 
     def _bn_common(self, d, op, n):
         x, m = op.x, op.m
@@ -858,7 +1015,11 @@ class Plan:
                         return [o]
 
                     self._contrib(x, em)
+            elif isinstance(op, AttnOp):
+                self._attn_backward(op, gout, gld)
             elif isinstance(op, FuseOp):
+                if op.detach:
+                    continue
                 for s in op.srcs:
                     if not s.buf.needs_grad:
                         continue
@@ -920,7 +1081,8 @@ class Plan:
             d.g_ld, d.x_ld = gld, x.buf.C
             d.n, d.oh, d.ow, d.cout = nb, out.H, out.W, lay.cout_p
             d.ih, d.iw, d.c, d.sy, d.sx = x.H, x.W, x.c, lay.stride, lay.stride
-            d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], 1, 1
+            d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], taps["ddy"], \
+                taps["ddx"]
             d.dtype = self.dt
             lib = L.load()
             hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))  # the halo kernel's preferred split

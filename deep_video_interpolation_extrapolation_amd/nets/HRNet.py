@@ -294,6 +294,12 @@ class HRNet(FlatParams, nn.Module):
                          requires_grad=vgrad)
         s1 = g.buffer("stem1", H, W, 64)
         g.conv(E.R(feat), self.conv1, E.R(s1), act=A.ACT_LRELU, cmap=self._stem_cmap(), name="conv1")
+        if getattr(self, "_export_stem", False):
+            # the stem concat [frames, seg_encoder(seg_k)...] as a detached NCHW side output
+            # (InterRefineNet's encoded_feat, nets/InterRefineNet.py:21-25)
+            g.export_nchw("stem_x", E.R(feat, 8 * F, rup(3 * F, 8)), 3 * F)
+            for k in range(F):
+                g.export_nchw(f"stem_seg{k}", E.R(feat, 8 * k, 4), 4)
         s2 = g.buffer("stem2", H, W, 64)
         g.conv(E.R(s1), self.conv2, E.R(s2), act=A.ACT_LRELU, name="conv2")
         x = E.R(s2)
@@ -441,9 +447,18 @@ class HRNet(FlatParams, nn.Module):
         g.output("segout", E.R(seg), self.seg_out_dim)
 
     def _build_plan(self, key):
-        n, H, W, dtype, train, dev, xgrad = key
-        g = self._lower(E.Graph(dtype), H, W, xgrad=xgrad, vgrad=bool(train))
+        n, H, W, dtype, train, dev, xgrad, export = key
+        self._export_stem = export
+        try:
+            g = self._lower(E.Graph(dtype), H, W, xgrad=xgrad, vgrad=bool(train))
+        finally:
+            self._export_stem = False
         return g.compile(n, dev, backward=train)
+
+    # set by InterRefineNet / InterStage3Net: every forward also writes the detached stem
+    # features [frames (3F), seg_encoder(seg_k) (4 each)] to `last_stem` (B, 7F, H, W)
+    export_stem = False
+    last_stem = None
 
     def _on_moved(self):
         self._pool.clear()
@@ -454,9 +469,16 @@ class HRNet(FlatParams, nn.Module):
         n, _, H, W = x.shape
         L.require_gpu(x)
         xgrad = bool(train) and bool(getattr(self, "_in_needs", (False,))[0])
-        plan = self._pool.acquire((n, H, W, self.dtype, bool(train), x.device, xgrad))
+        plan = self._pool.acquire((n, H, W, self.dtype, bool(train), x.device, xgrad, bool(self.export_stem)))
         plan.set_input("x", x)
         plan.set_input("seg", seg)
+        if self.export_stem:
+            F = self.n_frames
+            stem = torch.empty((n, 7 * F, H, W), dtype=torch.float32, device=x.device)
+            plan.set_output_nchw("stem_x", stem[:, :3 * F])
+            for k in range(F):
+                plan.set_output_nchw(f"stem_seg{k}", stem[:, 3 * F + 4 * k:3 * F + 4 * k + 4])
+            self.last_stem = stem
         if len(inputs) > 2:
             plan.set_input("vae", inputs[2])
         rgb = torch.empty((n, H, W, E.rup(self.rgb_out_dim, 8)), dtype=torch.float32, device=x.device)

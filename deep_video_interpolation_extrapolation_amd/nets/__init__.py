@@ -10,3 +10,5 @@ from .disc import (FrameDiscriminator, FrameLocalDiscriminator, FrameSNDiscrimin
                    VideoSNDiscriminator, VideoSNLocalDiscriminator)
 from .InterGANNet import InterGANNet, channel_softmax
 from .UNet import SegEncoder, SepUNet, UNet, double_conv, down, inconv, outconv, up
+from .refine import MSResAttnRefine, SRNRefine
+from .InterRefineNet import InterRefineNet, InterStage3Net

@@ -449,6 +449,58 @@ int dvie_reparam_bwd(const float* logvar, const float* eps, const float* gz, flo
                      int beta, void* stream);
 
 /*
+ * Local-window attention ops of the second-stage refinement nets (MSResAttnRefine,
+ * nets/refine_nets.py:138-399; corrmap l.253-287, weight_neighbors_by_probmap l.313-323,
+ * weight_neighbors_by_low_probmap l.289-311).  NHWC tensors of elem type dtype on an
+ * (n, h, w) grid; window entry k of a (wh x ww) window (both odd) is the neighbour at
+ * offset (k / ww - wh/2, k % ww - ww/2); the window weights of map m occupy channels
+ * [m*K, (m+1)*K), K = wh*ww; out-of-image neighbours read zero.
+ *   L2NORM      y[p, :c] = a[p, :c] / |a[p, :c]|                          (x / x.norm(dim=1))
+ *   L2NORM_BWD  y = (a - b0 <b0, a>) / |b1|      a = dL/dxn, b0 = xn, b1 = x
+ *   CORR        y[p, m*K + k] = <a[p, :c], b_m[p + o_k, :c]>, m < nhalf    (b_0 = b0, b_1 = b1;
+ *               a NULL map's entries are written as 0)
+ *   GATHER      y[p, :c] = sum_m sum_k a[p, (half0+m)*K + k] * b_m[p + o_k, :c]   (m < 1 + !!b1)
+ *   GATHER_T    y[q, :c] = sum_k a[q - o_k, half0*K + k] * b0[q - o_k, :c]  (adjoint in b)
+ *   SOFTMAX     y[p, :J] = softmax(a[p, :J]), J = nhalf*K
+ *   SOFTMAX_BWD y = b0 * (a - <b0, a>)           a = dL/dprob, b0 = prob
+ *   WNORM       per map: y = a / sum_k a
+ *   WNORM_BWD   per map: y = (a - <a, b0>) / sum_k b1     a = dL/dWn, b0 = Wn, b1 = W
+ *   POOL        y[p, :c] = mean of a over the in-image part of the centred (wh x ww) window
+ *               (F.avg_pool2d(k=(wh,ww), stride 1, pad (wh/2, ww/2), count_include_pad=False))
+ *   POOL_T      adjoint of POOL
+ * Then the common epilogue: v += res; v += y_old (beta); v = act(v); v *= act'(z) (dact).
+ * Vector ops (GATHER*, POOL*) need c, every ld % 4 == 0.
+ */
+#define DVIE_ATTN_L2NORM 0
+#define DVIE_ATTN_L2NORM_BWD 1
+#define DVIE_ATTN_CORR 2
+#define DVIE_ATTN_GATHER 3
+#define DVIE_ATTN_GATHER_T 4
+#define DVIE_ATTN_SOFTMAX 5
+#define DVIE_ATTN_SOFTMAX_BWD 6
+#define DVIE_ATTN_WNORM 7
+#define DVIE_ATTN_WNORM_BWD 8
+#define DVIE_ATTN_POOL 9
+#define DVIE_ATTN_POOL_T 10
+
+typedef struct dvie_attn_desc {
+  const void* a;
+  const void* b0;
+  const void* b1;
+  void* y;
+  const void* res;
+  const void* z;
+  long long a_ld, b_ld, y_ld, res_ld, z_ld;
+  int op, n, h, w;
+  int c, wh, ww, nhalf;
+  int half0, act, dact, beta;
+  int dtype, pad0;
+  float alpha, pad1;
+} dvie_attn_desc;
+
+int dvie_attn(const dvie_attn_desc* d, void* stream);
+
+/*
  * Op-list executor: runs n descriptors in order on one stream with a single host call
  * (the per-step forward and backward plans of the HRNet / VGG executors).
  */
@@ -463,6 +515,7 @@ int dvie_reparam_bwd(const float* logvar, const float* eps, const float* gz, flo
 #define DVIE_OP_BN_BWD 9
 #define DVIE_OP_HEAD_FWD 10
 #define DVIE_OP_HEAD_BWD 11
+#define DVIE_OP_ATTN 12
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
@@ -482,6 +535,7 @@ typedef struct dvie_op {
     dvie_pack_list pack;
     dvie_bn_desc bn;
     dvie_head_desc head;
+    dvie_attn_desc attn;
   } u;
 } dvie_op;
 

@@ -25,6 +25,9 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
                      body): loss dict, per-parameter gradient stats, post-Adamax checksums
   ckpt_manifest.json G10: the reference save_checkpoint dict (InterTrainer.py:867-885)
                      after the G4 step, written by torch.save and read back: its manifest
+  refine.npz     G11/G12: reference InterRefineNet (SRNRefine) and InterStage3Net
+                     (MSResAttnRefine, with / without stage3_prop), n_scales 2: outputs, flow
+                     maps, parameter-gradient stats for seeded output gradients
 """
 import os
 import sys
@@ -334,9 +337,55 @@ def g10():
         json.dump(man, f, indent=0, sort_keys=False)
 
 
+def _gstats(module):
+    named = dict(module.named_parameters())
+    names = sorted(n for n in named if named[n].grad is not None)
+    return np.array(names), np.array([[float(named[n].grad.double().sum()), float((named[n].grad.double() ** 2).sum())]
+                                      for n in names])
+
+
+def _flat_sample(t):
+    v = t.detach().double().reshape(-1)
+    return np.concatenate([[float(v.sum()), float(v.abs().sum()), float(v.norm())],
+                           v[inputs.sample_idx(v.numel())].numpy()])
+
+
+def g11():
+    """reference InterRefineNet (HRNet coarse + SRNRefine, n_scales 2; nets/InterRefineNet.py:8-28,
+    nets/refine_nets.py:27-135), train split, 32x64: forward outputs, and the refine net's
+    parameter gradients for seeded upstream gradients of every refine output; and G12:
+    InterStage3Net (+ MSResAttnRefine, refine_nets.py:138-399) at 64x128 with and without
+    stage3_prop: outputs, flow maps, stage-3 parameter gradients."""
+    out = {}
+    for tag, cls, H, W, prop in (("refine", "InterRefineNet", 32, 64, False), ("stage3", "InterStage3Net", 64, 128, False),
+                                 ("stage3prop", "InterStage3Net", 64, 128, True)):
+        args = args_ns(refine_model="SRNRefine", stage3_model="MSResAttnRefine", n_scales=2, split="train",
+                       with_gt_seg=False, stage3_prop=prop)
+        torch.manual_seed(1024)
+        m = ref_nets.__dict__[cls](args)
+        x, seg = inputs.hrnet_input(2, H, W)
+        res = m(x, seg=seg)
+        g = torch.Generator().manual_seed(91)
+        outs = list(res[2]) + (list(res[3]) if cls == "InterStage3Net" else [])
+        loss = sum((o * torch.randn(o.shape, generator=g)).sum() for o in outs)
+        loss.backward()
+        small = cls == "InterRefineNet"  # the 64x128 outputs are stored as stats + seeded samples
+        for i, o in enumerate(res[2]):
+            out[f"{tag}_refine{i}"] = o.detach().numpy() if small else _flat_sample(o)
+        if cls == "InterStage3Net":
+            for i, o in enumerate(res[3]):
+                out[f"{tag}_stage3_{i}"] = _flat_sample(o)
+            for i, f in enumerate(res[4]):
+                out[f"{tag}_flow{i}"] = f.numpy()
+            out[f"{tag}_names"], out[f"{tag}_grad_stats"] = _gstats(m.stage3_model)
+        out[f"{tag}_refine_names"], out[f"{tag}_refine_grad_stats"] = _gstats(m.refine_model)
+        _, out[f"{tag}_refine_init"] = checksums({k: v for k, v in m.refine_model.state_dict().items()})
+    np.savez_compressed(os.path.join(HERE, "refine.npz"), **out)
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()

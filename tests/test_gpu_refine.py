@@ -1,0 +1,199 @@
+"""GPU: the second-stage refinement nets on the HIP path against the CPU oracle
+(oracle/refine.py, pinned to the reference's InterRefineNet / InterStage3Net by G11/G12).
+
+* the local-window attention ops one by one in a small engine plan (L2 normalisation,
+  5x9 correlation over two maps, softmax over 90 entries, optional 3x5 pooling, weighted
+  gather, per-map normalised gather) with their backward, vs torch autograd in fp64;
+* SRNRefine and MSResAttnRefine (n_scales 1 / 2, stage3_prop off / on): outputs within
+  1e-4, parameter gradients by per-tensor relative L2 (LeakyReLU kinks, see
+  test_gpu_parity), flow maps;
+* InterRefineNet / InterStage3Net end to end against oracle.refine.inter_refine_forward;
+* the two-stage bf16 forward + backward at 1024x2048 (BASELINE config 5's frames).
+"""
+import numpy as np
+import pytest
+import torch
+
+import inputs
+from oracle import hrnet as OH
+from oracle import refine as OR
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / max(1e-30, float(b.norm())))
+
+
+def _args(**kw):
+    from deep_video_interpolation_extrapolation_amd.options import default_args
+    a = default_args("INTER", refine=True, refine_model="SRNRefine", precision="fp32", split="train")
+    a.__dict__.update(kw)
+    return a
+
+
+@pytest.mark.parametrize("prop", [False, True])
+def test_attention_ops_match_oracle(dev, prop):
+    """l2norm -> corr -> softmax (-> pool) -> gather / wnorm + per-map gather, fp32, vs the
+    oracle's corrmap / weighted_neighbours / weighted_neighbours_low in fp64: outputs 1e-5,
+    input gradients 1e-4 relative L2."""
+    from deep_video_interpolation_extrapolation_amd import engine as E
+    B, C, H, W = 2, 16, 7, 12
+    g = E.Graph(torch.float32)
+    X = {k: g.buffer(k, H, W, C) for k in ("x", "t1", "t2")}
+    for k, b in X.items():
+        g.input_nchw(E.R(b), k, ext_c=C, requires_grad=True)
+    n = {k: g.buffer(k + "n", H, W, C) for k in X}
+    for k in X:
+        g.l2norm(E.R(X[k]), E.R(n[k]))
+    NA = 92
+    sim = g.buffer("sim", H, W, NA)
+    g.corr(E.R(n["x"]), [E.R(n["t1"]), E.R(n["t2"])], E.R(sim), 5, 9)
+    prob = g.buffer("prob", H, W, NA)
+    g.softmax(E.R(sim), E.R(prob), 2, 5, 9)
+    if prop:
+        pp = g.buffer("pp", H, W, NA)
+        g.apool(E.R(prob), E.R(pp), 3, 5)
+        prob = pp
+    out = g.buffer("out", H, W, C)
+    g.gather(E.R(prob), [E.R(X["t1"]), E.R(X["t2"])], E.R(out), 0, 2, 5, 9)
+    wn = g.buffer("wn", H, W, NA)
+    g.wnorm(E.R(prob), E.R(wn), 2, 5, 9)
+    lf, lb = g.buffer("lf", H, W, C), g.buffer("lb", H, W, C)
+    g.gather(E.R(wn), [E.R(X["t1"])], E.R(lf), 0, 2, 5, 9)
+    g.gather(E.R(wn), [E.R(X["t2"])], E.R(lb), 1, 2, 5, 9)
+    for k, b in (("out", out), ("lf", lf), ("lb", lb)):
+        g.output_nchw(k, E.R(b), C)
+    plan = g.compile(B, dev, backward=True)
+    gen = torch.Generator().manual_seed(4)
+    ins = {k: torch.randn((B, C, H, W), generator=gen) for k in X}
+    gouts = {k: torch.randn((B, C, H, W), generator=gen) for k in ("out", "lf", "lb")}
+    dins = {k: t.to(dev) for k, t in ins.items()}  # the plan holds raw pointers: keep them alive
+    for k, t in dins.items():
+        plan.set_input(k, t)
+    outs = {k: torch.empty((B, C, H, W), device=dev) for k in gouts}
+    for k, t in outs.items():
+        plan.set_output_nchw(k, t)
+    plan.run_forward()
+    plan.set_param_grads()
+    dgouts = {k: t.to(dev) for k, t in gouts.items()}
+    for k, t in dgouts.items():
+        plan.set_output_grad(k, t)
+    gin = {k: torch.empty((B, C, H, W), device=dev) for k in ins}
+    for k, t in gin.items():
+        plan.set_input_grad(k, t)
+    plan.run_backward()
+    torch.cuda.synchronize()
+
+    r = {k: v.double().requires_grad_(True) for k, v in ins.items()}
+    p, _ = OR.corrmap(r["x"], r["t1"], r["t2"], prop)
+    ro = {"out": OR.weighted_neighbours(r["t1"], r["t2"], p)}
+    ro["lf"], ro["lb"] = OR.weighted_neighbours_low(r["t1"], r["t2"], p)
+    sum((ro[k] * gouts[k].double()).sum() for k in ro).backward()
+    for k in ro:
+        assert float((outs[k].cpu().double() - ro[k].detach()).abs().max()) < 1e-5, k
+    for k in r:
+        assert rel_l2(gin[k], r[k].grad) < 1e-4, (k, rel_l2(gin[k], r[k].grad))
+
+
+def _grads(P, names):
+    return {n: P[n].grad for n in names}
+
+
+@pytest.mark.parametrize("n_scales", [1, 2])
+def test_srn_refine_matches_oracle(dev, n_scales):
+    from deep_video_interpolation_extrapolation_amd import nets
+    H, W = 32, 64
+    torch.manual_seed(3)
+    m = nets.SRNRefine(_args(n_scales=n_scales)).to(dev)
+    P = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(8)
+    rgb = torch.rand((2, 3, H, W), generator=g) * 2 - 1
+    seg = torch.softmax(torch.randn((2, 20, H, W), generator=g), 1)
+    enc = torch.randn((2, 14, H, W), generator=g)
+    outs = m(rgb.to(dev), seg.to(dev), enc.to(dev))
+    gos = [torch.randn(o.shape, generator=g) for o in outs]
+    sum((o * go.to(dev)).sum() for o, go in zip(outs, gos)).backward()
+    torch.cuda.synchronize()
+    ref = OR.srn_forward(P, rgb, seg, enc, n_scales)
+    sum((o * go).sum() for o, go in zip(ref, gos)).backward()
+    assert len(outs) == n_scales
+    for o, r in zip(outs, ref):
+        assert o.shape == r.shape and float((o.detach().cpu() - r.detach()).abs().max()) < 1e-4
+    named = dict(m.named_parameters())
+    errs = [rel_l2(named[k].grad, P[k].grad) for k in P]
+    assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (float(np.median(errs)), max(errs))
+
+
+@pytest.mark.parametrize("prop", [False, True])
+def test_attn_refine_matches_oracle(dev, prop):
+    from deep_video_interpolation_extrapolation_amd import nets
+    H, W = 64, 128
+    torch.manual_seed(5)
+    m = nets.MSResAttnRefine(_args(n_scales=2, stage3_prop=prop)).to(dev)
+    P = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    img = torch.rand((2, 3, H, W), generator=g) * 2 - 1
+    seg = torch.softmax(torch.randn((2, 20, H, W), generator=g), 1)
+    x, nseg = inputs.hrnet_input(2, H, W)
+    outs, flows = m(img.to(dev), seg.to(dev), x.to(dev), nseg.to(dev))
+    gos = [torch.randn(o.shape, generator=g) for o in outs]
+    sum((o * go.to(dev)).sum() for o, go in zip(outs, gos)).backward()
+    torch.cuda.synchronize()
+    ref, rflows = OR.attn_forward(P, img, seg, x, nseg, 2, prop)
+    sum((o * go).sum() for o, go in zip(ref, gos)).backward()
+    for o, r in zip(outs, ref):
+        assert float((o.detach().cpu() - r.detach()).abs().max()) < 1e-4
+    for f, rf in zip(flows, rflows):
+        assert f.shape == rf.shape and float((f != rf).float().mean()) < 0.01
+    named = dict(m.named_parameters())
+    errs = [rel_l2(named[k].grad, P[k].grad) for k in P]
+    assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (float(np.median(errs)), max(errs))
+
+
+@pytest.mark.parametrize("stage3", [False, True])
+def test_two_stage_forward_matches_oracle(dev, stage3):
+    """InterRefineNet / InterStage3Net (HRNet coarse) at 64x128, n_scales 2: every output
+    within 1e-4 of oracle.refine.inter_refine_forward (seeded init identical to the
+    reference construction order, checked first)."""
+    from deep_video_interpolation_extrapolation_amd import nets
+    a = _args(n_scales=2, model="InterStage3Net" if stage3 else "InterRefineNet", stage3=stage3)
+    torch.manual_seed(1024)
+    m = (nets.InterStage3Net if stage3 else nets.InterRefineNet)(a).to(dev)
+    Pc = OH.init_params(1024)
+    Pr = OR.init_params(None, OR.srn_specs())
+    Ps = OR.init_params(None, OR.attn_specs()) if stage3 else None
+    for k, v in Pr.items():
+        assert torch.equal(m.refine_model.state_dict()[k].cpu(), v), k
+    x, seg = inputs.hrnet_input(2, 64, 128)
+    with torch.no_grad():
+        got = m(x.to(dev), seg=seg.to(dev))
+        ref = OR.inter_refine_forward(Pc, Pr, x, seg, 2, Ps=Ps)
+    assert float((got[0].cpu() - ref[0]).abs().max()) < 1e-4
+    for o, r in zip(got[2], ref[2]):
+        assert float((o.cpu() - r).abs().max()) < 1e-4
+    if stage3:
+        for o, r in zip(got[3], ref[3]):
+            assert float((o.cpu() - r).abs().max()) < 1e-4
+
+
+@pytest.mark.timeout(600)
+def test_two_stage_bf16_1024x2048(dev):
+    """BASELINE config 5 frames: InterStage3Net (HRNet + SRNRefine + MSResAttnRefine) bf16,
+    batch 1 at 1024x2048: forward + backward of the coarse + refine + stage-3 losses' stand-in
+    (sum of squares), every gradient finite and non-zero."""
+    from deep_video_interpolation_extrapolation_amd import nets
+    a = _args(n_scales=1, model="InterStage3Net", stage3=True, precision="bf16", train_coarse=True)
+    torch.manual_seed(1024)
+    m = nets.InterStage3Net(a).to(dev)
+    x, seg = inputs.hrnet_input(1, 1024, 2048)
+    c_rgb, c_seg, ref, re, flows = m(x.to(dev), seg=seg.to(dev))
+    loss = c_rgb.square().mean() + c_seg.square().mean() + sum(r.square().mean() for r in ref + re)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert np.isfinite(float(loss))
+    for mod in (m.coarse_model, m.refine_model, m.stage3_model):
+        fg = mod._flat_grad
+        assert bool(torch.isfinite(fg).all()) and float(fg.norm()) > 0, type(mod).__name__
+    assert flows[0].shape == (1, 2, 2, 256, 512)
