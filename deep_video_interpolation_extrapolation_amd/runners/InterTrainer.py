@@ -55,10 +55,19 @@ class InterTrainer:
             torch.cuda.set_device(self.device)
         self.log.info("Initializing trainer")
         model = get_model(args)
+        self.refine = bool(getattr(args, "refine", False))
+        self.stage3 = self.refine and bool(getattr(args, "stage3", False))
         if not getattr(args, "train_coarse", False):
             for p in model.coarse_model.parameters():
                 p.requires_grad = False
+        if self.refine and not getattr(args, "train_refine", False):  # reference l.49-51
+            for p in model.refine_model.parameters():
+                p.requires_grad = False
         self.log.info("coarse params " + str(count_parameters(model.coarse_model)))
+        if self.refine:
+            self.log.info("refine params " + str(count_parameters(model.refine_model)))
+            if self.stage3:
+                self.log.info("stage3 params " + str(count_parameters(model.stage3_model)))
         model.to(self.device)
         self.model = comm.GradSync(model)
         self.global_step = 0
@@ -67,8 +76,16 @@ class InterTrainer:
             self.train_set, self.val_set = get_dataset(args)
         if args.split == "train":
             self.RGBLoss = RGBLoss(args).to(self.device)
+            if self.refine:
+                self.refine_RGBLoss = RGBLoss(args, refine=True).to(self.device)
             self.SegLoss = SegCrossEntropy()
             self.coarse_opt = Adamax(list(self.model.module.coarse_model.parameters()), lr=args.coarse_learning_rate)
+            if self.refine:  # reference l.80-83
+                self.refine_opt = Adamax(list(self.model.module.refine_model.parameters()),
+                                         lr=args.refine_learning_rate)
+            if self.stage3:
+                self.stage3_opt = Adamax(list(self.model.module.stage3_model.parameters()),
+                                         lr=args.refine_learning_rate)
             if getattr(args, "clip_store", None):
                 self.train_loader = self._device_loader("train", shuffle=True)
             else:
@@ -108,28 +125,57 @@ class InterTrainer:
         seg = torch.cat([data["seg1"], data["seg3"]], dim=1) if self.args.mode == "xs2xs" else None
         return x, seg, gt_x, gt_seg
 
+    def _scale_gt(self, gt_x, i):
+        """refine_gt_x of reference l.418-419: gt at scale 1 / 2^(n_scales - i - 1)
+        (bilinear, align_corners=True)."""
+        n = self.args.n_scales
+        if i == n - 1:
+            return gt_x
+        return torch.nn.functional.interpolate(gt_x, scale_factor=1 / (2 ** (n - i - 1)), mode="bilinear",
+                                               align_corners=True)
+
     def step(self, data):
         """One training step (reference l.389-437).  data: sample dict (any device)."""
+        a = self.args
         data = batch_to(data, self.device)
         x, seg, gt_x, gt_seg = self.get_input(data)
         loss_dict = OrderedDict()
-        coarse_img, coarse_seg = self.model(x, seg=seg)
+        out = self.model(x, seg=seg)
+        coarse_img, coarse_seg = out[0], out[1]
         prefix = "coarse"
         loss_dict.update(self.RGBLoss(coarse_img, gt_x, False, prefix=prefix))
-        if self.args.mode == "xs2xs":
-            loss_dict[prefix + "_ce_loss"] = self.args.ce_weight * self.SegLoss(coarse_seg, gt_seg)
+        if a.mode == "xs2xs":
+            loss_dict[prefix + "_ce_loss"] = a.ce_weight * self.SegLoss(coarse_seg, gt_seg)
+        if self.refine:  # reference l.415-425 (per scale: refine, then stage 3)
+            refine_imgs = out[2]
+            stage3_imgs = out[3] if self.stage3 else None
+            for i in range(a.n_scales):
+                tag = str(1 / (2 ** (a.n_scales - i - 1)))
+                gts = self._scale_gt(gt_x, i)
+                loss_dict.update(self.refine_RGBLoss(refine_imgs[i], gts, False, prefix="refine_" + tag))
+                if self.stage3:
+                    loss_dict.update(self.refine_RGBLoss(stage3_imgs[i], gts, False, prefix="stage3_" + tag))
         loss = 0
         for v in loss_dict.values():
             loss = loss + torch.mean(v)
         loss_dict["loss_all"] = loss
-        self.coarse_opt.zero_grad(set_to_none=True)
+        for o in self._opts():
+            o.zero_grad(set_to_none=True)
         # reference `sync` divides loss_all by W in place before backward (l.431, 859-864)
         (loss / self.W).backward()
         self.model.finish()
-        if getattr(self.args, "train_coarse", False):
+        if getattr(a, "train_coarse", False):
             self.coarse_opt.step()
+        if self.refine and getattr(a, "train_refine", False):
+            self.refine_opt.step()
+        if self.stage3 and getattr(a, "train_stage3", False):
+            self.stage3_opt.step()
         self.global_step += 1
         return comm.sync_losses(OrderedDict((k, v.detach()) for k, v in loss_dict.items()), self.W)
+
+    def _opts(self):
+        return [self.coarse_opt] + ([self.refine_opt] if self.refine else []) + ([self.stage3_opt] if self.stage3
+                                                                                 else [])
 
     # ---------------- loops ----------------
     def set_epoch(self, epoch):
@@ -177,12 +223,19 @@ class InterTrainer:
         self.log.info("Validation epoch {} started".format(self.epoch))
         self.model.eval()
         crit = ["coarse_l1", "coarse_psnr", "coarse_ssim", "coarse_vgg"] + (["coarse_iou"] if self.args.mode == "xs2xs" else [])
+        if self.refine:  # reference l.568-569
+            crit += ["refine_l1", "refine_psnr", "refine_ssim", "refine_vgg"]
         meters = {c: AverageMeter() for c in crit}
         with torch.no_grad():
             for i, data in enumerate(self.val_loader):
                 data = batch_to(data, self.device)
                 x, seg, gt_x, gt_seg = self.get_input(data)
-                coarse_img, coarse_seg = self._predict(x, seg, gt_x, gt_seg)
+                refine_img = None
+                if self.refine:  # reference l.593-598
+                    out = self.model(x, seg=seg, gt_seg=gt_seg)
+                    coarse_img, coarse_seg, refine_img = out[0], out[1], out[2][-1].clamp(-1, 1)
+                else:
+                    coarse_img, coarse_seg = self._predict(x, seg, gt_x, gt_seg)
                 coarse_img = coarse_img.clamp(-1, 1)
                 a, b = self.normalize(coarse_img), self.normalize(gt_x)
                 d = OrderedDict()
@@ -192,6 +245,12 @@ class InterTrainer:
                 if self.args.mode == "xs2xs":
                     d["coarse_iou"] = self.IoULoss.of_scores(coarse_seg, gt_seg)  # IoU(argmax, argmax), fused
                 d["coarse_vgg"] = self.VGGCosLoss(a, b, False)
+                if refine_img is not None:  # reference l.625-633
+                    r = self.normalize(refine_img)
+                    d["refine_l1"] = self.L1Loss(r, b)
+                    d["refine_psnr"] = self.PSNRLoss(r, b)
+                    d["refine_ssim"] = 1 - self.SSIMLoss(r, b)
+                    d["refine_vgg"] = self.VGGCosLoss(r, b, False)
                 d = comm.sync_losses(d, self.W)
                 if self.rank == 0:
                     for c in crit:
@@ -217,9 +276,16 @@ class InterTrainer:
         name = self._ckpt_name(self.args.model, self.args.session, self.epoch, getattr(self, "step_idx", 0),
                                self.args.path)
         os.makedirs(os.path.dirname(name), exist_ok=True)
-        torch.save({"session": self.args.session, "epoch": self.epoch + 1,
-                    "coarse_model": self.model.module.coarse_model.state_dict(),
-                    "coarse_opt": self.coarse_opt.state_dict()}, name)
+        d = {"session": self.args.session, "epoch": self.epoch + 1,
+             "coarse_model": self.model.module.coarse_model.state_dict(),
+             "coarse_opt": self.coarse_opt.state_dict()}
+        if self.refine:  # reference l.879-884
+            d["refine_model"] = self.model.module.refine_model.state_dict()
+            d["refine_opt"] = self.refine_opt.state_dict()
+            if self.stage3:
+                d["stage3_model"] = self.model.module.stage3_model.state_dict()
+                d["stage3_opt"] = self.stage3_opt.state_dict()
+        torch.save(d, name)
         self.log.info("save model: {}".format(name))
         return name
 
@@ -229,12 +295,19 @@ class InterTrainer:
         self.log.info("Loading checkpoint %s" % name)
         ckpt = torch.load(name, map_location="cpu", weights_only=True)
         # weights gated by load_coarse, optimizer state by train_coarse and load_coarse (l.902-936)
-        if getattr(a, "load_coarse", False):
-            sd = self.model.module.coarse_model.state_dict()
-            sd.update(ckpt["coarse_model"])
-            self.model.module.coarse_model.load_state_dict(sd)
-        if a.split == "train" and getattr(a, "train_coarse", False) and getattr(a, "load_coarse", False):
-            self.coarse_opt.load_state_dict(ckpt["coarse_opt"])
+        m = self.model.module
+        for part in ("coarse", "refine", "stage3"):
+            if not getattr(a, "load_" + part, False):
+                continue
+            assert part == "coarse" or getattr(a, part if part == "stage3" else "refine", False), \
+                "--load_%s needs --%s" % (part, part)
+            sd = getattr(m, part + "_model").state_dict()
+            sd.update(ckpt[part + "_model"])
+            getattr(m, part + "_model").load_state_dict(sd)
+        if a.split == "train":  # optimizer states (l.929-952)
+            for part in ("coarse", "refine", "stage3"):
+                if getattr(a, "train_" + part, False) and getattr(a, "load_" + part, False):
+                    getattr(self, part + "_opt").load_state_dict(ckpt[part + "_opt"])
         # epoch bookkeeping as the reference (l.953-958): the file's epoch is checkepoch + 1
         if getattr(a, "resume", False):
             assert ckpt["epoch"] - 1 == a.checkepoch, [ckpt["epoch"], a.checkepoch]

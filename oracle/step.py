@@ -147,3 +147,39 @@ def extra_rollout_step(params, vgg_state, data, nps=2, lr=1e-3, weights=(80.0, 8
     grads = {k: v.grad.detach().clone() for k, v in P.items()}
     new, state = adamax(params, grads, lr)
     return OrderedDict((k, float(v)) for k, v in ld.items()), grads, new
+
+
+def refine_step(Pc, Pr, vgg_state, data, n_scales, Ps=None, prop=False, lr=1e-3,
+                weights=(80.0, 80.0, 20.0, 20.0, 30.0), rweights=(80.0, 80.0, 20.0, 20.0)):
+    """One InterTrainer step with --refine [--stage3] (reference runners/InterTrainer.py:
+    396-439): coarse RGBLoss + CE, then per scale i the refine RGBLoss (and the stage-3
+    one) against gt resized by 1 / 2^(n_scales - 1 - i) (bilinear, align_corners=True),
+    prefixes 'refine_<scale>' / 'stage3_<scale>'; one backward; Adamax on every part.
+    Returns (loss dict, grads per part, new params per part)."""
+    import torch.nn.functional as F
+    from . import refine as R
+    parts = {"coarse": Pc, "refine": Pr}
+    if Ps is not None:
+        parts["stage3"] = Ps
+    P = {k: {n: v.detach().clone().requires_grad_(True) for n, v in d.items()} for k, d in parts.items()}
+    gt_x, gt_seg = data["frame2"], data["seg2"]
+    x = torch.cat([data["frame1"], data["frame3"]], 1)
+    seg = torch.cat([data["seg1"], data["seg3"]], 1)
+    res = R.inter_refine_forward(P["coarse"], P["refine"], x, seg, n_scales, Ps=P.get("stage3"), prop=prop)
+    ld = losses.rgb_loss(vgg_state, res[0], gt_x, normed=False, w=weights[:4])
+    ld["coarse_ce_loss"] = weights[4] * losses.seg_ce(res[1], gt_seg)
+    for i in range(n_scales):
+        tag = str(1 / (2 ** (n_scales - i - 1)))
+        gts = gt_x if i == n_scales - 1 else F.interpolate(gt_x, scale_factor=1 / (2 ** (n_scales - i - 1)),
+                                                            mode="bilinear", align_corners=True)
+        ld.update(losses.rgb_loss(vgg_state, res[2][i], gts, normed=False, w=rweights, prefix="refine_" + tag))
+        if Ps is not None:
+            ld.update(losses.rgb_loss(vgg_state, res[3][i], gts, normed=False, w=rweights, prefix="stage3_" + tag))
+    loss = 0
+    for v in ld.values():
+        loss = loss + torch.mean(v)
+    ld["loss_all"] = loss
+    loss.backward()
+    grads = {k: {n: v.grad.detach().clone() for n, v in d.items()} for k, d in P.items()}
+    new = {k: adamax(parts[k], grads[k], lr)[0] for k in parts}
+    return OrderedDict((k, float(v.detach())) for k, v in ld.items()), grads, new

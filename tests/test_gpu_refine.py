@@ -197,3 +197,34 @@ def test_two_stage_bf16_1024x2048(dev):
         fg = mod._flat_grad
         assert bool(torch.isfinite(fg).all()) and float(fg.norm()) > 0, type(mod).__name__
     assert flows[0].shape == (1, 2, 2, 256, 512)
+
+
+@pytest.mark.timeout(300)
+def test_inter_trainer_stage3_step_matches_oracle(dev):
+    """InterTrainer --refine --stage3 (InterStage3Net, n_scales 2) fp32 step at 64x128 vs
+    oracle.step.refine_step: loss dict (coarse, refine_<scale>, stage3_<scale> keys in the
+    reference order) within 1e-4; gradients of all three nets by per-tensor relative L2;
+    post-Adamax weights (fraction moved differently)."""
+    from deep_video_interpolation_extrapolation_amd.runners.InterTrainer import InterTrainer
+    from oracle import losses as OL
+    from oracle import step as OS
+    a = _args(model="InterStage3Net", refine=True, stage3=True, train_coarse=True, train_refine=True,
+              train_stage3=True, n_scales=2, batch_size=2, input_h=64, input_w=128, synthetic=2, num_workers=0)
+    torch.manual_seed(1024)
+    tr = InterTrainer(a)
+    data = OS.synthetic_batch(2, 64, 128)
+    ld = tr.step(data)
+    Pc = OH.init_params(1024)
+    Pr = OR.init_params(None, OR.srn_specs())
+    Ps = OR.init_params(None, OR.attn_specs())
+    ref, grads, new = OS.refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps)
+    assert list(ld.keys()) == list(ref.keys()), (list(ld.keys()), list(ref.keys()))
+    np.testing.assert_allclose([float(ld[k]) for k in ref], [ref[k] for k in ref], rtol=1e-4)
+    m = tr.model.module
+    for part, mod in (("coarse", m.coarse_model), ("refine", m.refine_model), ("stage3", m.stage3_model)):
+        named = dict(mod.named_parameters())
+        errs = [rel_l2(named[k].grad, g) for k, g in grads[part].items()]
+        assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (part, float(np.median(errs)), max(errs))
+        moved = sum(int(((named[k].detach().cpu() - w).abs() > 1e-4).sum()) for k, w in new[part].items())
+        total = sum(w.numel() for w in new[part].values())
+        assert moved <= 1e-3 * total, (part, moved, total)
