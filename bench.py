@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
     ap.add_argument("--ops-out", default=None, help="write the per-op profile table (profiling steps) here")
+    ap.add_argument("--graph", type=int, default=1, help="1: time the hipGraph-captured step (runners/graph.py), "
+                                                           "0: the eager step")
     return ap.parse_args()
 
 
@@ -62,22 +64,41 @@ def make_batch(n, H, W, device, first):
     return {k: torch.stack([it[k] for it in items]).to(device) for k in items[0]}
 
 
-def cpu_baseline(H, W):
-    """CPU oracle step (reference algorithm, fp32) on a bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(H, W, steps=2):
+    """CPU oracle InterTrainer steps (the reference algorithm restated in PyTorch-CPU fp32)
+    on bounded samples, BASELINE.md's CPU plan: one untimed warm-up step, then
+    * the bench workload's frame size (H x W, batch 2): `steps` timed steps -> value;
+    * C1 (8 triplets at 128x256, batch 2 = 4 steps), timed whole -> c1_frames_per_s."""
     from oracle import hrnet, losses, step
     threads = torch.get_num_threads()
     P = hrnet.init_params(1024)
     vs = losses.synthetic_vgg19_state()
-    warm = step.synthetic_batch(1, 64, 128)
-    step.inter_step(P, vs, warm)
+    step.inter_step(P, vs, step.synthetic_batch(2, 64, 128))  # warm-up (untimed)
     B = 2
-    data = step.synthetic_batch(B, H, W)
     t = time.time()
-    step.inter_step(P, vs, data)
+    for k in range(steps):
+        step.inter_step(P, vs, step.synthetic_batch(B, H, W, first_index=B * k))
     dt = time.time() - t
-    return {"value": B / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"1 InterTrainer step of the CPU oracle (fp32) at {H}x{W}, batch {B}, after a 64x128 warm-up; "
-                      f"{dt:.1f}s"}
+    t1 = time.time()
+    for k in range(4):
+        step.inter_step(P, vs, step.synthetic_batch(2, 128, 256, first_index=2 * k))
+    dt1 = time.time() - t1
+    return {"value": B * steps / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "os_cpu_count": os.cpu_count(), "torch_threads": threads, "cpu_model": _cpu_model(),
+            "c1_frames_per_s": round(8 / dt1, 4),
+            "sample": f"{steps} InterTrainer steps of the CPU oracle (fp32) at {H}x{W}, batch {B} ({dt:.1f}s), after "
+                      f"one untimed warm-up step; C1: 8 triplets at 128x256 in 4 steps of batch 2 ({dt1:.1f}s)"}
 
 
 def warp_roofline(dev, n, H, W, reps=20):
@@ -209,24 +230,33 @@ def main():
     trainer = InterTrainer(args)
     data = make_batch(a.batch, a.height, a.width, dev, rank * a.batch)
 
+    def timed(fn):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            out = fn(data)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t)
+        return dt, out
+
     for _ in range(a.warmup):
         trainer.step(data)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        ld = trainer.step(data)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t)
+    eager_dt, ld = timed(trainer.step)
+    dt = eager_dt
+    if a.graph:
+        from deep_video_interpolation_extrapolation_amd.runners.graph import GraphedStep
+        gstep = GraphedStep(trainer, data, warmup=1)  # the batch now lives in the graph's static inputs
+        dt, ld = timed(lambda _d: gstep.step())
     loss_all = float(ld["loss_all"])
 
     # ---- profiling steps: per-op HIP events on the launch stream ----
@@ -304,7 +334,9 @@ def main():
             "dtype": a.precision,
             "data": "synthetic (seeded Cityscapes-shaped triplets, HBM-resident); random-init HRNet, synthetic VGG19",
             "config": {"workload": f"InterNet int_5_len_3 train step {a.height}x{a.width} {a.precision}",
-                       "per_gpu_batch": a.batch, "global_batch": a.batch * world, "parallelism": f"dp{world}"},
+                       "per_gpu_batch": a.batch, "global_batch": a.batch * world, "parallelism": f"dp{world}",
+                       "step": "hipGraph-captured" if a.graph else "eager"},
+            "eager_ms_per_step": round(eager_dt * 1e3 / a.steps, 3),
             "roofline": roof,
             "loss_all": loss_all,
             "step_breakdown_ms": {k: round(v["ms"] / max(1, a.profile_steps), 3) for k, v in sorted(agg.items())},

@@ -199,7 +199,8 @@ EXPORTS = [
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
-    "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn",
+    "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
+    "dvie_adam_dev",
 ]
 
 _lib = None
@@ -250,6 +251,10 @@ def load():
         lib.dvie_adamax.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
         lib.dvie_scale.argtypes = [vp, i64, f32, vp]
         lib.dvie_adam.argtypes = [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, vp]
+        f64 = ctypes.c_double
+        lib.dvie_adamax_dev.argtypes = [vp, vp, vp, vp, i64, f64, f64, f64, f64, f64, vp, vp]
+        lib.dvie_adam_dev.argtypes = [vp, vp, vp, vp, i64, f64, f64, f64, f64, f64, vp, vp]
+        lib.dvie_step_inc.argtypes = [vp, vp]
         for name in ("dvie_sn_fwd", "dvie_sn_bwd"):
             getattr(lib, name).argtypes = [vp, i32, vp, vp]
             getattr(lib, name).restype = i32

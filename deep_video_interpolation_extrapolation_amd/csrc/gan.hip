@@ -284,7 +284,11 @@ __global__ void softmax_bwd_kernel(dvie_softmax_desc d) {
 // p -= step_size * m / (sqrt(v) + eps), step_size = lr*sqrt(1-b2^t)/(1-b1^t) (host).
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, long long n, float step_size, float b1, float b2, float eps,
-                            float wd) {
+                            float wd, const float* __restrict__ stepp, double lr, double b1d, double b2d) {
+  if (stepp) {  // device-resident step count (graph-captured steps), host-identical doubles
+    const double t = (double)stepp[0];
+    step_size = (float)(lr * sqrt(1.0 - pow(b2d, t)) / (1.0 - pow(b1d, t)));
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float pv = p[i];
     float gr = g[i];
@@ -422,7 +426,16 @@ int dvie_adam(float* p, const float* g, float* m, float* v, long long n, float s
   DVIE_CHECK_ARG(p && g && m && v && n >= 0, "adam: args");
   if (n == 0) return DVIE_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, step_size, b1,
-                     b2, eps, wd);
+                     b2, eps, wd, (const float*)nullptr, 0.0, 0.0, 0.0);
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_adam_dev(float* p, const float* g, float* m, float* v, long long n, double lr, double b1, double b2,
+                  double eps, double wd, const float* step, void* stream) {
+  DVIE_CHECK_ARG(p && g && m && v && step && n >= 0, "adam_dev: args");
+  if (n == 0) return DVIE_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, 0.f,
+                     (float)b1, (float)b2, (float)eps, (float)wd, step, lr, b1, b2);
   DVIE_RETURN_LAUNCH();
 }
 

@@ -288,7 +288,10 @@ __global__ __launch_bounds__(256) void warp_bwd_flow_kernel(const dvie_warp_desc
 
 __global__ void adamax_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                               float* __restrict__ u, long long n, float clr, float b1, float b2, float eps,
-                              float wd) {
+                              float wd, const float* __restrict__ stepp, double lr, double b1d) {
+  // device-resident step count (graph-captured steps): clr = lr / (1 - b1^t) in double
+  // from the caller's double lr / beta1, exactly as the host computes it for an eager step
+  if (stepp) clr = (float)(lr / (1.0 - pow(b1d, (double)stepp[0])));
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float gr = g[i];
     const float pv = p[i];
@@ -302,6 +305,11 @@ __global__ void adamax_kernel(float* __restrict__ p, const float* __restrict__ g
     u[i] = un;
     p[i] = pv - clr * (mn / un);
   }
+}
+
+// one-element increment of a device step counter (thread-indexed: a vector store)
+__global__ void step_inc_kernel(float* step) {
+  if (threadIdx.x == 0) step[threadIdx.x] += 1.f;
 }
 
 __global__ void scale_kernel(float* p, long long n, float s) {
@@ -352,7 +360,22 @@ int dvie_adamax(float* p, const float* g, float* m, float* u, long long n, float
   DVIE_CHECK_ARG(p && g && m && u && n >= 0, "adamax: args");
   if (n == 0) return DVIE_OK;
   hipLaunchKernelGGL(adamax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, u, n, clr, b1, b2,
-                     eps, wd);
+                     eps, wd, (const float*)nullptr, 0.0, 0.0);
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_adamax_dev(float* p, const float* g, float* m, float* u, long long n, double lr, double b1, double b2,
+                    double eps, double wd, const float* step, void* stream) {
+  DVIE_CHECK_ARG(p && g && m && u && step && n >= 0, "adamax_dev: args");
+  if (n == 0) return DVIE_OK;
+  hipLaunchKernelGGL(adamax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, u, n, 0.f,
+                     (float)b1, (float)b2, (float)eps, (float)wd, step, lr, b1);
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_step_inc(float* step, void* stream) {
+  DVIE_CHECK_ARG(step, "step_inc: null");
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step);
   DVIE_RETURN_LAUNCH();
 }
 

@@ -402,14 +402,15 @@ class MSResAttnRefine(FlatParams, nn.Module):
     def flow_maps(plan):
         """corrmap's flow maps (refine_nets.py:273-279) from the similarity buffers of the
         last forward: per map, window argmax k -> (k // h, k % h) - (w//2, h//2), the
-        reference's own index decomposition; CPU float (B, 2, 2, h, w)."""
+        reference's own index decomposition; float (B, 2, 2, h, w).  They stay on the
+        device (the reference moves them to the CPU; a device-to-host copy inside a step
+        would break its hipGraph capture): callers that visualise them call .cpu()."""
         flows = []
         for sim in plan.sims:
-            t = sim.buf.t[..., :2 * WH * WW].float()
+            t = sim.buf.t[..., :2 * WH * WW]
             n, h, w = t.shape[:3]
-            idx = t.view(n, h, w, 2, WH * WW).argmax(-1).permute(0, 3, 1, 2)  # (B, 2, h, w)
-            f = torch.stack([idx // WH, idx % WH], 2).float().cpu()
-            flows.append(f - torch.tensor([WW // 2, WH // 2], dtype=torch.float32).view(1, 1, 2, 1, 1))
+            idx = t.reshape(n, h, w, 2, WH * WW).argmax(-1).permute(0, 3, 1, 2)  # (B, 2, h, w)
+            flows.append(torch.stack([idx // WH - WW // 2, idx % WH - WH // 2], 2).float())
         return flows
 
     def forward(self, coarse_img, coarse_seg, neighbors_img, neighbors_seg):

@@ -27,9 +27,36 @@ class _FusedOptimizer(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self._flat = {}
+        self.capturable = False
+        self._dsteps = {}
 
     def _launch(self, p, g, s0, s1, n, group, step, device):
         raise NotImplementedError
+
+    def _launch_dev(self, p, g, s0, s1, n, group, dstep, device):
+        raise NotImplementedError
+
+    def set_capturable(self, flag=True):
+        """Graph capture (runners/graph.py): keep every step count on the device and
+        compute the bias correction there, so a captured step replays correctly.  The
+        first step after switching must run eagerly (it moves the counts)."""
+        self.capturable = bool(flag)
+        if not flag:
+            for st in self.state.values():
+                if "step" in st and torch.is_tensor(st["step"]) and st["step"].is_cuda:
+                    st["step"] = st["step"].detach().cpu().clone()
+            self._dsteps = {}
+
+    def _dev_step(self, key, params, device):
+        """one device step tensor shared by `params` (created from their host count)"""
+        d = self._dsteps.get(key)
+        if d is None or d.device != device:
+            st = self.state[params[0]]
+            d = torch.full((1,), float(st.get("step", 0.0)), dtype=torch.float32, device=device)
+            self._dsteps[key] = d
+        for p in params:
+            self.state[p]["step"] = d
+        return d
 
     def _flat_group(self, gi, group):
         """(owner, flat state 0, flat state 1) if the group maps onto one flat buffer."""
@@ -47,7 +74,8 @@ class _FusedOptimizer(torch.optim.Optimizer):
             g = p.grad
             if g is None or g.data_ptr() != fg.data_ptr() + (p.data_ptr() - flat.data_ptr()):
                 return None
-        if len({float(self.state[p]["step"]) if "step" in self.state[p] else 0.0 for p in ps}) > 1:
+        if not self.capturable and len({float(self.state[p]["step"]) if "step" in self.state[p] else 0.0
+                                        for p in ps}) > 1:
             return None  # per-parameter step counts differ (SN u, v become trainable after step 1)
         k0, k1 = self.STATE
         ent = self._flat.get(gi)
@@ -76,6 +104,14 @@ class _FusedOptimizer(torch.optim.Optimizer):
         k0, k1 = self.STATE
         for gi, group in enumerate(self.param_groups):
             flat = self._flat_group(gi, group)
+            if flat is not None and self.capturable:
+                owner, m, u = flat
+                lib, s = L.load(), L.stream_ptr(owner._flat.device)
+                dstep = self._dev_step(("g", gi), group["params"], owner._flat.device)
+                L.check(lib.dvie_step_inc(dstep.data_ptr(), s), "step count")
+                self._launch_dev(owner._flat, owner._flat_grad, m, u, owner._flat.numel(), group, dstep,
+                                 owner._flat.device)
+                continue
             if flat is not None:
                 owner, m, u = flat
                 ps = group["params"]
@@ -94,15 +130,21 @@ class _FusedOptimizer(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st[k0] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st[k1] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
                 g = p.grad.contiguous()
                 assert p.is_contiguous() and st[k0].is_contiguous()
+                if self.capturable:
+                    dstep = self._dev_step(("p", id(p)), [p], p.device)
+                    L.check(L.load().dvie_step_inc(dstep.data_ptr(), L.stream_ptr(p.device)), "step count")
+                    self._launch_dev(p, g, st[k0], st[k1], p.numel(), group, dstep, p.device)
+                    continue
+                st["step"] += 1
                 self._launch(p, g, st[k0], st[k1], p.numel(), group, float(st["step"]), p.device)
         return loss
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._flat = {}  # re-bind flat state views (copies loaded values in _flat_group)
+        self._dsteps = {}
 
 
 class Adamax(_FusedOptimizer):
@@ -116,6 +158,12 @@ class Adamax(_FusedOptimizer):
         clr = group["lr"] / (1 - b1 ** step)
         L.check(L.load().dvie_adamax(p.data_ptr(), g.data_ptr(), s0.data_ptr(), s1.data_ptr(), n, clr, b1, b2,
                                      group["eps"], group["weight_decay"], L.stream_ptr(device)), "adamax")
+
+    def _launch_dev(self, p, g, s0, s1, n, group, dstep, device):
+        b1, b2 = group["betas"]
+        L.check(L.load().dvie_adamax_dev(p.data_ptr(), g.data_ptr(), s0.data_ptr(), s1.data_ptr(), n, group["lr"], b1,
+                                         b2, group["eps"], group["weight_decay"], dstep.data_ptr(),
+                                         L.stream_ptr(device)), "adamax")
 
 
 class Adam(_FusedOptimizer):
@@ -131,3 +179,9 @@ class Adam(_FusedOptimizer):
         step_size = group["lr"] * math.sqrt(1 - b2 ** step) / (1 - b1 ** step)
         L.check(L.load().dvie_adam(p.data_ptr(), g.data_ptr(), s0.data_ptr(), s1.data_ptr(), n, step_size, b1, b2,
                                    group["eps"], group["weight_decay"], L.stream_ptr(device)), "adam")
+
+    def _launch_dev(self, p, g, s0, s1, n, group, dstep, device):
+        b1, b2 = group["betas"]
+        L.check(L.load().dvie_adam_dev(p.data_ptr(), g.data_ptr(), s0.data_ptr(), s1.data_ptr(), n, group["lr"], b1, b2,
+                                       group["eps"], group["weight_decay"], dstep.data_ptr(), L.stream_ptr(device)),
+                "adam")

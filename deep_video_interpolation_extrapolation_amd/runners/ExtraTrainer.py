@@ -52,8 +52,9 @@ class ExtraTrainer(InterTrainer):
         gt_seg = [data["seg" + str(i + 3)] if self.args.mode == "xs2xs" else None for i in range(vl)]
         return x, seg, gt_x, gt_seg
 
-    def step(self, data):
-        """One training step (reference l.249-323)."""
+    def forward_backward(self, data):
+        """Forward, losses and backward of one step (reference l.249-317); the gradient
+        all-reduce and Adamax follow in InterTrainer.apply_gradients."""
         a = self.args
         npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
         if nps > 1:
@@ -61,7 +62,7 @@ class ExtraTrainer(InterTrainer):
         data = batch_to(data, self.device)
         # a rollout runs HRNet's backward nps times into one flat gradient: reduce it once,
         # after the last backward (see GradSync.set_overlap)
-        self.model.set_overlap(nps == 1)
+        self.model.set_overlap(nps == 1 and not getattr(self, "no_overlap", False))
         xs2xs = a.mode == "xs2xs"
         loss_dict = OrderedDict()
         last_rgb = torch.cat([data["frame1"], data["frame2"]], dim=1)
@@ -95,11 +96,7 @@ class ExtraTrainer(InterTrainer):
         loss_dict["loss_all"] = loss
         self.coarse_opt.zero_grad(set_to_none=True)
         (loss / self.W).backward()  # reference `sync` divides loss_all by W in place (l.317, 760-765)
-        self.model.finish()
-        if getattr(a, "train_coarse", False):
-            self.coarse_opt.step()
-        self.global_step += 1
-        return comm.sync_losses(OrderedDict((k, v.detach()) for k, v in loss_dict.items()), self.W)
+        return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
 
     def validate(self):
         """Reference l.421-583: per (step, frame) L1 / PSNR / SSIM / IoU / VGG-cos."""

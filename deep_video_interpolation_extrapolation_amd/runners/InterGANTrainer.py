@@ -66,7 +66,9 @@ class InterGANTrainer(InterTrainer):
         out = self.model(x, seg, gt_x, gt_seg)
         return out[0], out[1]
 
-    def step(self, data):
+    def forward_backward(self, data):
+        """InterGANNet forward, losses and one backward of their sum (reference
+        l.359-442); apply_gradients runs the all-reduce and the optimizers."""
         a = self.args
         data = batch_to(data, self.device)
         x, seg, gt_x, gt_seg = self.get_input(data)
@@ -94,19 +96,28 @@ class InterGANTrainer(InterTrainer):
         for v in loss_dict.values():
             loss = loss + torch.mean(v)
         loss_dict["loss_all"] = loss
-        opts = self._opts()
-        for o in opts.values():
+        for o in self._gan_opts().values():
             o.zero_grad(set_to_none=True)
         (loss / self.W).backward()  # reference `sync` divides loss_all by W in place (l.442, 902-907)
-        self.model.finish()
+        return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
+
+    def apply_gradients(self, reduce=True):
+        a = self.args
+        if reduce:
+            self.model.finish()
+        else:
+            self.model.scale()
+        opts = self._gan_opts()
         if getattr(a, "train_coarse", False):
             self.coarse_opt.step()
         for kind in ("frame_disc", "video_disc"):
             if getattr(a, kind, False) and getattr(a, "train_" + kind, False) and self.global_step > GAN_TRAIN_STEP:
                 opts[kind].step()
-        return comm.sync_losses(OrderedDict((k, v.detach()) for k, v in loss_dict.items()), self.W)
 
     def _opts(self):
+        return list(self._gan_opts().values())
+
+    def _gan_opts(self):
         o = OrderedDict(coarse=self.coarse_opt)
         if hasattr(self, "frame_disc_opt"):
             o["frame_disc"] = self.frame_disc_opt

@@ -136,6 +136,29 @@ class InterTrainer:
 
     def step(self, data):
         """One training step (reference l.389-437).  data: sample dict (any device)."""
+        ld = self.forward_backward(data)
+        self.apply_gradients()
+        return comm.sync_losses(ld, self.W)
+
+    def apply_gradients(self, reduce=True):
+        """Gradient all-reduce (+ 1/W) and the optimizer steps.  reduce=False: the 1/W
+        scale and the optimizers only (device work: runners/graph.py captures it after an
+        eager GradSync.reduce())."""
+        a = self.args
+        if reduce:
+            self.model.finish()
+        else:
+            self.model.scale()
+        if getattr(a, "train_coarse", False):
+            self.coarse_opt.step()
+        if self.refine and getattr(a, "train_refine", False):
+            self.refine_opt.step()
+        if self.stage3 and getattr(a, "train_stage3", False):
+            self.stage3_opt.step()
+        self.global_step += 1
+
+    def forward_backward(self, data):
+        """Forward, losses and backward of one step -> detached loss dict (this rank's)."""
         a = self.args
         data = batch_to(data, self.device)
         x, seg, gt_x, gt_seg = self.get_input(data)
@@ -163,15 +186,7 @@ class InterTrainer:
             o.zero_grad(set_to_none=True)
         # reference `sync` divides loss_all by W in place before backward (l.431, 859-864)
         (loss / self.W).backward()
-        self.model.finish()
-        if getattr(a, "train_coarse", False):
-            self.coarse_opt.step()
-        if self.refine and getattr(a, "train_refine", False):
-            self.refine_opt.step()
-        if self.stage3 and getattr(a, "train_stage3", False):
-            self.stage3_opt.step()
-        self.global_step += 1
-        return comm.sync_losses(OrderedDict((k, v.detach()) for k, v in loss_dict.items()), self.W)
+        return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
 
     def _opts(self):
         return [self.coarse_opt] + ([self.refine_opt] if self.refine else []) + ([self.stage3_opt] if self.stage3

@@ -86,10 +86,22 @@ class GradSync:
         """Wait for the bucket all-reduces and apply the 1/W factor (HIP kernel)."""
         if self.W == 1:
             return
+        self.reduce()
+        self.scale()
+
+    def reduce(self):
+        """The collectives of finish(): the post-backward all-reduces, then wait for all."""
+        if self.W == 1:
+            return
         for m in (self.post if self.overlap else self.flat_owners):
             if m._flat_grad is not None and any(p.grad is not None for p in m.parameters()):
                 self.works.append(dist.all_reduce(m._flat_grad, op=dist.ReduceOp.SUM, async_op=True))
         self.wait()
+
+    def scale(self):
+        """The 1/W factor of finish() (device work only: graph-capturable)."""
+        if self.W == 1:
+            return
         lib = L.load()
         for m in self.flat_owners:
             g = m._flat_grad

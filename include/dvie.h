@@ -317,6 +317,16 @@ size_t dvie_warp_ws_floats(const dvie_warp_desc* d);
 int dvie_adamax(float* p, const float* g, float* m, float* u, long long n, float clr,
                 float b1, float b2, float eps, float wd, void* stream);
 
+/*
+ * Graph-capturable variants (the step count lives on the device, so a captured step
+ * replays with the right bias correction): dvie_step_inc adds 1 to *step; dvie_adamax_dev
+ * computes clr = lr / (1 - b1^(*step)) on the device in double from the double lr / b1 a
+ * host would use, then updates as dvie_adamax (elementwise math in float, as there).
+ */
+int dvie_step_inc(float* step, void* stream);
+int dvie_adamax_dev(float* p, const float* g, float* m, float* u, long long n, double lr, double b1, double b2,
+                    double eps, double wd, const float* step, void* stream);
+
 /* scale a flat fp32 buffer in place (used for the 1/W gradient factor) */
 int dvie_scale(float* p, long long n, float s, void* stream);
 
@@ -405,6 +415,9 @@ int dvie_softmax_bwd(const dvie_softmax_desc* d, void* stream);
  */
 int dvie_adam(float* p, const float* g, float* m, float* v, long long n, float step_size, float b1, float b2,
               float eps, float wd, void* stream);
+/* the same with step_size computed on the device from lr and *step (graph-captured steps) */
+int dvie_adam_dev(float* p, const float* g, float* m, float* v, long long n, double lr, double b1, double b2,
+                  double eps, double wd, const float* step, void* stream);
 
 /*
  * SpectralNorm (reference nets/SpectralNorm.py:10-68), fp32, one workgroup per layer.

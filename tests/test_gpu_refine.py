@@ -146,7 +146,7 @@ def test_attn_refine_matches_oracle(dev, prop):
     for o, r in zip(outs, ref):
         assert float((o.detach().cpu() - r.detach()).abs().max()) < 1e-4
     for f, rf in zip(flows, rflows):
-        assert f.shape == rf.shape and float((f != rf).float().mean()) < 0.01
+        assert f.shape == rf.shape and float((f.cpu() != rf).float().mean()) < 0.01
     named = dict(m.named_parameters())
     errs = [rel_l2(named[k].grad, P[k].grad) for k in P]
     assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (float(np.median(errs)), max(errs))
