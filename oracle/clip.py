@@ -8,7 +8,9 @@ restated with the same library calls it makes.
   frame, torchvision F.crop(img, top=h1, left=w1, h, w) == PIL img.crop((w1, h1, w1+w, h1+h)),
   to_tensor (HWC uint8 -> CHW float / 255), normalize((.5,)*3, (.5,)*3), and
   np.eye(20)[seg] transposed to (20, h, w) float.
-Parity: pinned by construction to those PIL / numpy / torch calls; the reference
+Parity: seq_crop_params and draw_flip are pinned to the reference itself (fixture G13,
+tests/golden/clip_crops.npz, generated from folder.py:125-149, 166); prep_clip is pinned by
+construction to those PIL / numpy / torch calls; the reference
 DatasetFolder itself is not executed (its torchvision transforms are absent offline).
 """
 import random

@@ -28,6 +28,8 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
   refine.npz     G11/G12: reference InterRefineNet (SRNRefine) and InterStage3Net
                      (MSResAttnRefine, with / without stage3_prop), n_scales 2: outputs, flow
                      maps, parameter-gradient stats for seeded output gradients
+  clip_crops.npz G13: reference get_seq_crop_params (folder.py:125-149) crops and the
+                     flip draw (folder.py:211) for seeds 0..63
 """
 import os
 import sys
@@ -383,9 +385,25 @@ def g11():
     np.savez_compressed(os.path.join(HERE, "refine.npz"), **out)
 
 
+def g12():
+    """reference folder.py:125-149 get_seq_crop_params (the pseudo-motion crops of the
+    Cityscapes clip loader; it reads no instance state) for np.random seeds 0..63, and the
+    horizontal-flip draw of folder.py:211 (random.randint(0, 2)) for random seeds 0..63."""
+    import random
+    import folder as ref_folder  # reference folder.py
+    cls = next(v for v in vars(ref_folder).values() if isinstance(v, type) and hasattr(v, "get_seq_crop_params"))
+    crops, flips = [], []
+    for seed in range(64):
+        np.random.seed(seed)
+        crops.append([list(c) for c in cls.get_seq_crop_params(None)])
+        random.seed(seed)
+        flips.append(ref_folder.randint(0, 2))
+    np.savez_compressed(os.path.join(HERE, "clip_crops.npz"), crops=np.array(crops), flips=np.array(flips))
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11, g12)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()
