@@ -51,7 +51,7 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     args.rank, args.gpus = rank, world
-    if args.resume or args.split != "train":
+    if args.resume or args.split != "train":  # reference main.py:127 (cycgen writes under load_dir)
         args.path = args.load_dir
     else:
         args.path = get_exp_path(args)
@@ -90,8 +90,12 @@ def main(argv=None):
             trainer.train()
             if rank == 0:
                 trainer.save_checkpoint()
-    else:
-        raise NotImplementedError(f"split {args.split}: needs the Cityscapes clips on disk (SURVEY §8f)")
+    elif args.split == "cycgen":  # reference main.py:108-110
+        assert args.cycgen_load_dir is not None, "please specify cycgen load dir where to load data"
+        trainer.cycgen()
+    else:  # 'test' / 'mycycgen'
+        raise NotImplementedError(f"split {args.split}: the reference's trainers define no test() "
+                                  "(its main.py:96-97 raises AttributeError there)")
     if world > 1:
         dist.destroy_process_group()
 

@@ -147,34 +147,6 @@ class ExtraTrainer(InterTrainer):
             self._scalars("val/score", res)
         return res
 
-    def mini_test(self, img_list, seg_list):
-        """Reference l.681-757: autoregressive rollout from two [0,1] frames (and one-hot or
-        label segmentations).  Returns per-step predicted images in [0,1] and label maps."""
-        assert len(img_list) == 2 and len(seg_list) == 2
-        if seg_list[0].dim() == 3:
-            seg_list = [torch.nn.functional.one_hot(s.long(), 20).permute(0, 3, 1, 2).float() for s in seg_list]
-        self.model.eval()
-        dev = self.device
-        a = self.args
-        npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
-        pred_img, pred_seg = [], []
-        with torch.no_grad():
-            i1, i2 = img_list[0].to(dev) * 2 - 1, img_list[1].to(dev) * 2 - 1
-            s1, s2 = seg_list[0].to(dev), seg_list[1].to(dev)
-            for _ in range(nps):
-                img, seg = self.model(torch.cat([i1, i2], 1), torch.cat([s1, s2], 1))[:2]
-                for j in range(npo):
-                    pred_img.append(self.normalize(img[:, 3 * j:3 * j + 3]))
-                    pred_seg.append(torch.argmax(seg[:, 20 * j:20 * j + 20], dim=1))
-                if npo == 1:
-                    i1, i2 = i2, pred_img[-1] * 2 - 1
-                    s1, s2 = s2, onehot_argmax(seg[:, :20])
-                else:
-                    i1, i2 = pred_img[-2] * 2 - 1, pred_img[-1] * 2 - 1
-                    s1 = torch.nn.functional.one_hot(pred_seg[-2], 20).permute(0, 3, 1, 2).float()
-                    s2 = torch.nn.functional.one_hot(pred_seg[-1], 20).permute(0, 3, 1, 2).float()
-        return [p.cpu() for p in pred_img], [s.cpu() for s in pred_seg]
-
     def save_checkpoint(self):
         return super().save_checkpoint()
 

@@ -276,6 +276,76 @@ class InterTrainer:
             self._scalars("val/score", res)
         return res
 
+    def mini_test(self, img_list, seg_list):
+        """Autoregressive rollout from two [0, 1] frames and their segmentations (one-hot
+        (B, 20, H, W) or label (B, H, W)) -> per predicted frame the image in [0, 1] and the
+        label map, on the CPU (reference InterTrainer.py:786-856 / ExtraTrainer.py:681-757;
+        num_pred_step / num_pred_once default to 1 where the runner's options lack them)."""
+        assert len(img_list) == 2 and len(seg_list) == 2
+        if seg_list[0].dim() == 3:
+            seg_list = [torch.nn.functional.one_hot(s.long(), 20).permute(0, 3, 1, 2).float() for s in seg_list]
+        self.model.eval()
+        dev = self.device
+        a = self.args
+        npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
+        onehot = lambda lab: torch.nn.functional.one_hot(lab, 20).permute(0, 3, 1, 2).float()  # noqa: E731
+        pred_img, pred_seg = [], []
+        with torch.no_grad():
+            i1, i2 = img_list[0].to(dev) * 2 - 1, img_list[1].to(dev) * 2 - 1
+            s1, s2 = seg_list[0].to(dev), seg_list[1].to(dev)
+            for _ in range(nps):
+                out = self.model(torch.cat([i1, i2], 1), seg=torch.cat([s1, s2], 1))
+                img, seg = out[0], out[1]
+                for j in range(npo):
+                    pred_img.append(self.normalize(img[:, 3 * j:3 * j + 3]))
+                    pred_seg.append(torch.argmax(seg[:, 20 * j:20 * j + 20], dim=1))
+                if npo == 1:
+                    i1, i2 = i2, pred_img[-1] * 2 - 1
+                    s1, s2 = s2, onehot(pred_seg[-1])
+                else:
+                    i1, i2 = pred_img[-2] * 2 - 1, pred_img[-1] * 2 - 1
+                    s1, s2 = onehot(pred_seg[-2]), onehot(pred_seg[-1])
+        return [p.cpu() for p in pred_img], [s.cpu() for s in pred_seg]
+
+    def cycgen(self):
+        """--split cycgen (reference InterTrainer.py:691-784 / ExtraTrainer.py:586-679): for
+        each clip directory, frames 00.0 and {interval}.0 (rgb/ and seg/ PNGs under
+        --cycgen_load_dir) -> mini_test rollout -> the inputs and predictions saved as rgb,
+        seg and palette-coloured vis_seg PNGs under
+        <path>/cycgen/cityscape/<H>x<W>/extra_int_<interval>_len_<vid_length>_nearest/.
+        The clip list: the first 61 clip directories in sorted order (the reference reads it
+        from a pickle at an absolute path of its authors' machine, root_clip.pkl 'val'[:61])."""
+        import numpy as np
+        from PIL import Image
+        from ..utils.net_utils import save_image, vis_seg_mask
+        a = self.args
+        assert self.rank == 0, "cycgen runs on one worker"
+        assert a.cycgen_load_dir is not None, "please specify --cycgen_load_dir"
+        interval = int(a.interval)
+        split = "extra_int_{}_len_{}_nearest".format(interval, a.vid_length)
+        root = os.path.join(a.path, "cycgen", "cityscape", "{}x{}".format(a.input_h, a.input_w), split)
+        load_img_dir, load_seg_dir = os.path.join(a.cycgen_load_dir, "rgb"), os.path.join(a.cycgen_load_dir, "seg")
+        clips = sorted(d for d in os.listdir(load_img_dir) if os.path.isdir(os.path.join(load_img_dir, d)))[:61]
+        idx = ["{:0>2d}.0".format(0), "{:0>2d}.0".format(interval)]
+        for clip in clips:
+            imgs = [torch.from_numpy(np.asarray(Image.open(os.path.join(load_img_dir, clip, i + ".png")).convert("RGB"),
+                                                dtype=np.float32) / 255).permute(2, 0, 1).unsqueeze(0) for i in idx]
+            labs = [torch.from_numpy(np.asarray(Image.open(os.path.join(load_seg_dir, clip, i + ".png")).convert("L"),
+                                                dtype=np.int64)).unsqueeze(0) for i in idx]
+            segs = [torch.nn.functional.one_hot(l_, 20).permute(0, 3, 1, 2).float() for l_ in labs]
+            p_img, p_seg = self.mini_test(imgs, segs)
+            save_img = imgs + p_img
+            save_seg = [s.argmax(dim=1) for s in segs] + p_seg
+            save_vis = [vis_seg_mask(torch.nn.functional.one_hot(s, 20).permute(0, 3, 1, 2).float(), 20)
+                        for s in save_seg]
+            names = ["{:0>2d}.0".format(int(i * interval)) for i in range(a.vid_length + 2)]
+            for sub, lst in (("rgb", save_img), ("seg", save_seg), ("vis_seg", save_vis)):
+                d = os.path.join(root, sub, clip)
+                os.makedirs(d, exist_ok=True)
+                for k in range(a.vid_length + 2):
+                    save_image(lst[k].squeeze(0), os.path.join(d, names[k] + ".png"))
+        return root
+
     def _scalars(self, tag, info):
         path = getattr(self.args, "path", None)
         if path:

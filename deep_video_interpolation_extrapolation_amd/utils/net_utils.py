@@ -94,3 +94,35 @@ class AverageMeter:
         self.sum += val * n
         self.count += n
         self.avg = self.sum / self.count
+
+
+# the Cityscapes 19-class palette + "none" (reference utils/data_utils.py:86-107)
+CITYSCAPES_COLORS = [
+    (128, 64, 128), (244, 35, 232), (70, 70, 70), (102, 102, 156), (190, 153, 153), (153, 153, 153),
+    (250, 170, 30), (220, 220, 0), (107, 142, 35), (152, 251, 152), (70, 130, 180), (220, 20, 60),
+    (255, 0, 0), (0, 0, 142), (0, 0, 70), (0, 60, 100), (0, 80, 100), (0, 0, 230), (119, 11, 32), (0, 0, 0),
+]
+
+
+def vis_seg_mask(seg, n_classes, seg_id=False):
+    """(B, C, H, W) scores (or (B, 1, H, W) ids with seg_id) -> (B, 3, H, W) palette colours
+    in [0, 1] (reference utils/net_utils.py:57-70)."""
+    assert seg.dim() == 4
+    ids = seg.squeeze(1).long() if seg_id else seg.argmax(1)
+    pal = torch.tensor(CITYSCAPES_COLORS, dtype=torch.float32, device=seg.device)
+    return pal[ids].permute(0, 3, 1, 2).contiguous() / 255
+
+
+def save_image(t, path):
+    """torchvision.utils.save_image of one image (reference's save calls): (C, H, W) or
+    (H, W) values scaled by 255, +0.5, clamped to [0, 255], a 1-channel image repeated to
+    RGB, written as PNG."""
+    import numpy as np
+    from PIL import Image
+    t = t.detach().float().cpu()
+    if t.dim() == 2:
+        t = t.unsqueeze(0)
+    if t.shape[0] == 1:
+        t = t.repeat(3, 1, 1)
+    arr = t.mul(255).add(0.5).clamp(0, 255).to(torch.uint8).permute(1, 2, 0).numpy()
+    Image.fromarray(np.ascontiguousarray(arr)).save(path)

@@ -135,3 +135,34 @@ def test_im2col_head_dgrad_matches_halo_path(dev):
     assert torch.isfinite(g1).all()
     rel = float((g1 - g0).norm() / g0.norm())
     assert rel < 1e-2, rel
+
+
+def test_main_launcher_cycgen(dev, tmp_path):
+    """--split cycgen (reference main.py:107-109, ExtraTrainer.py:586-679): one EXTRA
+    training epoch on synthetic clips, then the rollout generation from a directory of
+    rgb/seg PNG clips with the saved checkpoint: inputs + predictions written as rgb / seg /
+    vis_seg PNGs at the input size."""
+    from PIL import Image
+    from deep_video_interpolation_extrapolation_amd import main as M
+    common = ["--syn_type", "extra", "--bs", "2", "--input_h", "32", "--input_w", "64", "--epochs", "1",
+              "--save_dir", str(tmp_path / "log"), "--synthetic", "2", "--nw", "0", "--precision", "fp32"]
+    M.main(common + ["EXTRA", "--train_coarse"])
+    run = next((tmp_path / "log").iterdir())
+    ck = next((run / "checkpoint").iterdir())
+    cyc = tmp_path / "cyc"
+    rng = np.random.RandomState(0)
+    for clip in ("aachen_000001", "bochum_000002"):
+        for sub in ("rgb", "seg"):
+            (cyc / sub / clip).mkdir(parents=True)
+        for idx in ("00.0", "01.0"):
+            Image.fromarray(rng.randint(0, 256, (32, 64, 3), dtype=np.uint8)).save(cyc / "rgb" / clip / f"{idx}.png")
+            Image.fromarray(rng.randint(0, 20, (32, 64), dtype=np.uint8)).save(cyc / "seg" / clip / f"{idx}.png")
+    M.main(common + ["--split", "cycgen", "--load_dir", str(run), "--checkepoch", "1", "--checkpoint",
+                     ck.name.split("_")[-1][:-4], "--checksession", "0", "--cycgen_load_dir", str(cyc), "EXTRA",
+                     "--load_coarse"])
+    out = run / "cycgen" / "cityscape" / "32x64" / "extra_int_1_len_1_nearest"
+    for sub in ("rgb", "seg", "vis_seg"):
+        for clip in ("aachen_000001", "bochum_000002"):
+            names = sorted(p.name for p in (out / sub / clip).iterdir())
+            assert names == ["00.0.png", "01.0.png", "02.0.png"], (sub, clip, names)
+            assert Image.open(out / sub / clip / "02.0.png").size == (64, 32)
