@@ -514,15 +514,17 @@ static int env_cfg() {
 // weights of its 32 output channels for all 9 taps in VGPRs (loaded once per workgroup), so
 // the tap loop reads only input-halo fragments from LDS and needs no barrier; one barrier
 // per output tile (halo double buffer).  8 waves = 2 channel halves x 4 output rows.
-template <int KS, bool OUTF32>
-__global__ __launch_bounds__(512) void conv_ws_kernel(const dvie_conv_desc p, int n_tiles, int tiles_x, int tiles_y,
-                                                      int persistent) {
-  typedef HaloCfg<1, 2, 4, 3, 3> C;  // halo geometry of a 4-row x 64-pixel tile, 8 waves
-  constexpr int NW = 8;
+// WP = output rows per tile: 4 (8 waves, one workgroup per CU) or 2 (4 waves, two
+// workgroups per CU: twice the independent halo streams in flight per CU).
+template <int KS, bool OUTF32, int WP>
+__global__ __launch_bounds__(2 * WP * 64, 4 / WP) void conv_ws_kernel(const dvie_conv_desc p, int n_tiles,
+                                                                       int tiles_x, int tiles_y, int persistent) {
+  typedef HaloCfg<1, 2, WP, 3, 3> C;  // halo geometry of a WP-row x 64-pixel tile, 2*WP waves
+  constexpr int NW = 2 * WP;
   __shared__ __attribute__((aligned(1024))) char smem[2 * C::HSZ];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave >> 2, wp = wave & 3;
+  const int wc = wave / WP, wp = wave % WP;
   const int r32 = lane & 31, hh = lane >> 5;
   const unsigned OOB = 0xFFFFFFF0u;
 
@@ -730,18 +732,31 @@ __global__ __launch_bounds__(512) void conv_ws_kernel(const dvie_conv_desc p, in
   }
 }
 
+template <int KS, int WP>
+static void launch_ws_rows(const dvie_conv_desc& p, hipStream_t s) {
+  const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + WP - 1) / WP;
+  const int n_tiles = tiles_x * tiles_y * p.n;
+  const int cap = 256 * (4 / WP);  // resident workgroups: one (WP 4) or two (WP 2) per CU
+  const int persistent = n_tiles > cap ? 1 : 0;
+  const int grid = persistent ? cap : n_tiles;
+  if (p.out_f32)
+    hipLaunchKernelGGL((conv_ws_kernel<KS, true, WP>), dim3(grid), dim3(2 * WP * 64), 0, s, p, n_tiles, tiles_x,
+                       tiles_y, persistent);
+  else
+    hipLaunchKernelGGL((conv_ws_kernel<KS, false, WP>), dim3(grid), dim3(2 * WP * 64), 0, s, p, n_tiles, tiles_x,
+                       tiles_y, persistent);
+}
+
+// tuning knob (read once): DVIE_WS_ROWS = 2 (default: two workgroups per CU, +1.3% step
+// same-box A/B 192.8-193.1 vs 190.5 frames/s, profiles/r02_ab/ab_wsrows.txt) or 4
+static const int ws_rows = getenv("DVIE_WS_ROWS") && atoi(getenv("DVIE_WS_ROWS")) == 4 ? 4 : 2;
+
 template <int KS>
 static void launch_ws(const dvie_conv_desc& p, hipStream_t s) {
-  const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + 3) / 4;
-  const int n_tiles = tiles_x * tiles_y * p.n;
-  const int persistent = n_tiles > 256 ? 1 : 0;
-  const int grid = persistent ? 256 : n_tiles;
-  if (p.out_f32)
-    hipLaunchKernelGGL((conv_ws_kernel<KS, true>), dim3(grid), dim3(512), 0, s, p, n_tiles, tiles_x, tiles_y,
-                       persistent);
+  if (ws_rows == 2)
+    launch_ws_rows<KS, 2>(p, s);
   else
-    hipLaunchKernelGGL((conv_ws_kernel<KS, false>), dim3(grid), dim3(512), 0, s, p, n_tiles, tiles_x, tiles_y,
-                       persistent);
+    launch_ws_rows<KS, 4>(p, s);
 }
 
 // Returns true when the halo kernel took the launch.
