@@ -124,6 +124,8 @@ def warp_roofline(dev, n, H, W, reps=20):
     d = L.WarpDesc()
     d.img, d.flow, d.out, d.dout, d.dimg, d.dflow = (t.data_ptr() for t in (x, flow, out, go, dx, dflow))
     d.n, d.c, d.h, d.w, d.align_corners = n, 3, H, W, 1
+    ws = torch.empty(lib.dvie_warp_ws_floats(ctypes.byref(d)), device=dev)
+    d.ws = ws.data_ptr()
     s = L.stream_ptr(dev)
 
     def fwd():

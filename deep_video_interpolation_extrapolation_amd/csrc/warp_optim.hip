@@ -3,6 +3,10 @@
 //
 // Reference: FlowWrapper utils/net_utils.py:89-114 (warp / warp_back l.116-129);
 // torch.optim.Adamax at runners/InterTrainer.py:79.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
 
 namespace dvie {
@@ -51,12 +55,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t warp_plane(const float* im, lo
 }
 
 // the four corner values, zero where the corner lies outside the image: an invalid corner
-// gets an out-of-range buffer offset, so the hardware returns 0 and all four loads issue
-// unconditionally, back to back (a zero corner adds +0, exactly as the skipped term would)
+// gets an out-of-range buffer offset, so the hardware returns 0 (a zero corner adds +0,
+// exactly as the skipped term would)
+// pair = (wave-uniform) every lane's two columns lie inside the image
 __device__ __forceinline__ void warp_corners(__amdgpu_buffer_rsrc_t im, const WarpTap& t, int w, float& a, float& b,
-                                             float& c, float& d) {
+                                             float& c, float& d, bool pair = false) {
   constexpr unsigned kOut = 0x80000000u;
   const unsigned r0 = (unsigned)(t.y0 * w), r1 = (unsigned)((t.y0 + 1) * w);
+  if (pair) {
+    // one 8-byte load per corner row (the vector-memory pipe, not the bytes, bounds these
+    // gathers: one instruction per row instead of two)
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(im, t.vy0 ? (r0 + t.x0) * 4u : kOut, 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(im, t.vy1 ? (r1 + t.x0) * 4u : kOut, 0, 0);
+    a = __uint_as_float(u[0]);
+    b = __uint_as_float(u[1]);
+    c = __uint_as_float(v[0]);
+    d = __uint_as_float(v[1]);
+    return;
+  }
   const unsigned oa = (t.vy0 && t.vx0) ? (r0 + t.x0) * 4u : kOut;
   const unsigned ob = (t.vy0 && t.vx1) ? (r0 + t.x0 + 1) * 4u : kOut;
   const unsigned oc = (t.vy1 && t.vx0) ? (r1 + t.x0) * 4u : kOut;
@@ -67,9 +83,7 @@ __device__ __forceinline__ void warp_corners(__amdgpu_buffer_rsrc_t im, const Wa
   d = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(im, od, 0, 0));
 }
 
-__device__ __forceinline__ float warp_sample(__amdgpu_buffer_rsrc_t im, const WarpTap& t, int w) {
-  float a, b, c, d;
-  warp_corners(im, t, w, a, b, c, d);
+__device__ __forceinline__ float warp_blend(float a, float b, float c, float d, const WarpTap& t) {
   float v = 0.f;
   v += a * t.wnw;
   v += b * t.wne;
@@ -78,9 +92,15 @@ __device__ __forceinline__ float warp_sample(__amdgpu_buffer_rsrc_t im, const Wa
   return v;
 }
 
-// A wave covers 256 consecutive pixels of one row, 4 per lane 64 apart: each gather
-// instruction then reads the sources of 64 consecutive output pixels (a few cache lines for
-// a smooth flow), and the flow loads and output stores are 256-byte coalesced runs.
+// These kernels are latency-bound gathers: a wave's time is its chain of dependent memory
+// round trips, not its bytes.  So each kernel issues every load it can before the first use
+// -- all channels of all its pixels at once (CC = the channel count as a compile-time
+// constant; CC = 0 is the generic per-channel loop) -- and stores only after the loads.
+//
+// Forward: a wave covers 256 consecutive pixels of one row, 4 per lane 64 apart: each gather
+// instruction reads the sources of 64 consecutive output pixels (a few cache lines for a
+// smooth flow), and the flow loads and output stores are 256-byte coalesced runs.
+template <int CC>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
   const int segs = (p.w + 255) >> 8;
   const long long hw = (long long)p.h * p.w;
@@ -92,40 +112,70 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
     const int sg = wv % segs;
     const int r = wv / segs;
     const int y = r % p.h, n = r / p.h;
-    WarpTap t[4];
-    bool live[4];
+    const __amdgpu_buffer_rsrc_t rf0 = warp_plane(p.flow + (long long)n * 2 * hw, hw);
+    const __amdgpu_buffer_rsrc_t rf1 = warp_plane(p.flow + ((long long)n * 2 + 1) * hw, hw);
+    float fx[4], fy[4];
+    bool live[4], pair[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int x = (sg << 8) + lane + 64 * k;
       live[k] = x < p.w;
-      const int xl = live[k] ? x : p.w - 1;  // clamped: the loads stay unconditional
-      const long long fo = (long long)y * p.w + xl;
-      t[k] = warp_tap(xl, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo], p.w, p.h,
-                      p.align_corners);
+      const unsigned fo = (unsigned)(y * p.w + (live[k] ? x : p.w - 1)) * 4u;  // clamped: loads stay unconditional
+      fx[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf0, fo, 0, 0));
+      fy[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf1, fo, 0, 0));
     }
-    for (int c = 0; c < p.c; ++c) {
-      const long long plane = ((long long)n * p.c + c) * hw;
-      const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + plane, hw), out = warp_plane(p.out + plane, hw);
-      float o[4];
+    WarpTap t[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = warp_sample(im, t[k], p.w);
+    for (int k = 0; k < 4; ++k) {
+      const int x = (sg << 8) + lane + 64 * k;
+      t[k] = warp_tap(live[k] ? x : p.w - 1, y, fx[k], fy[k], p.w, p.h, p.align_corners);
+      pair[k] = __all(t[k].vx0 && t[k].vx1);
+    }
+    auto store = [&](int c, const float* o) {
+      const __amdgpu_buffer_rsrc_t out = warp_plane(p.out + ((long long)n * p.c + c) * hw, hw);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {  // columns past the row end: out-of-range offset, store dropped
         const unsigned off = live[k] ? (unsigned)(y * p.w + (sg << 8) + lane + 64 * k) * 4u : 0x80000000u;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[k]), out, off, 0, 0);
+      }
+    };
+    if constexpr (CC > 0) {
+      float v[CC][4][4];
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + ((long long)n * CC + c) * hw, hw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) warp_corners(im, t[k], p.w, v[c][k][0], v[c][k][1], v[c][k][2], v[c][k][3], pair[k]);
+      }
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = warp_blend(v[c][k][0], v[c][k][1], v[c][k][2], v[c][k][3], t[k]);
+        store(c, o);
+      }
+    } else {
+      for (int c = 0; c < p.c; ++c) {
+        const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + ((long long)n * p.c + c) * hw, hw);
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float a, b, cc, d;
+          warp_corners(im, t[k], p.w, a, b, cc, d, pair[k]);
+          o[k] = warp_blend(a, b, cc, d, t[k]);
+        }
+        store(c, o);
       }
     }
   }
 }
 
 // ---- backward ----
-// d/d(img) of one bilinear corner, and the flow-gradient terms, per channel (order of the
-// reference autograd: corners nw, ne, sw, se)
-template <typename Scatter>
-__device__ __forceinline__ void warp_bwd_pixel(float a, float b, float c, float d, float go, const WarpTap& t,
-                                               float& gix, float& giy, Scatter&& scatter) {
+// the flow-gradient terms of one channel (order of the reference autograd: corners nw, ne,
+// sw, se); invalid corners contribute exact zeros (their value is 0)
+__device__ __forceinline__ void warp_dflow_terms(float a, float b, float c, float d, float go, const WarpTap& t,
+                                                 float& gix, float& giy) {
   const int x1 = t.x0 + 1, y1 = t.y0 + 1;
-  // invalid corners contribute exact zeros to the flow terms (their value is 0)
   gix -= a * ((float)y1 - t.iy) * go;
   giy -= a * ((float)x1 - t.ix) * go;
   gix += b * ((float)y1 - t.iy) * go;
@@ -134,155 +184,302 @@ __device__ __forceinline__ void warp_bwd_pixel(float a, float b, float c, float 
   giy += c * ((float)x1 - t.ix) * go;
   gix += d * (t.iy - (float)t.y0) * go;
   giy += d * (t.ix - (float)t.x0) * go;
-  if (t.vy0 && t.vx0) scatter(t.y0, t.x0, t.wnw * go);
-  if (t.vy0 && t.vx1) scatter(t.y0, x1, t.wne * go);
-  if (t.vy1 && t.vx0) scatter(y1, t.x0, t.wsw * go);
-  if (t.vy1 && t.vx1) scatter(y1, x1, t.wse * go);
-}
-
-__device__ __forceinline__ void warp_store_dflow(const dvie_warp_desc& p, int n, long long fo, float gix, float giy) {
-  const long long hw = (long long)p.h * p.w;
-  const float sx = p.align_corners ? (float)(p.w - 1) / 2.f : (float)p.w / 2.f;
-  const float sy = p.align_corners ? (float)(p.h - 1) / 2.f : (float)p.h / 2.f;
-  p.dflow[((long long)n * 2 + 0) * hw + fo] = -gix * sx;
-  p.dflow[((long long)n * 2 + 1) * hw + fo] = -giy * sy;
 }
 
 // Image gradient by gathering instead of scattering (LDS float atomics measured at ~100
 // cycles per wave instruction on gfx950, global ones at ~100 G lanes/s: both far below HBM).
 // A dimg pixel c receives the bilinear weight of every sample s (output pixel) that has c as
-// a corner.  Under a smooth flow those samples sit next to s*(c) = c - d(c), d(c) being the
-// integer source displacement (x0 - x, y0 - y) of the sample AT c.  warp_bwd_pull_kernel
-// visits the 4x4 candidates s*(c) + [-2, 1]^2 for every c and STORES dimg (no zero-fill, no
-// atomics, a fixed summation order); warp_bwd_flow_kernel computes dflow and adds, with a
-// global atomic, each (s, c) pair the candidate rule misses (folding / discontinuous flow).
-constexpr int WP_LO = -2, WP_HI = 1;
+// a corner: x0(s) in {cx - 1, cx} and y0(s) in {cy - 1, cy}.  Write x0(s) = sx + D(s), D the
+// integer part of the sample's displacement; where D(s) = D(c) the samples are
+// sx in {o.x - 1, o.x}, o = 2c - (x0, y0)(c).  The pull window of c, per axis, is
+//   WIN = 4: o.x + {-2 .. 1}: every sample with |delta(s) - delta(c)| < 1 px;
+//   WIN = 3: the side the fractional part f(c) = ix(c) - x0(c) points to, o.x + {-1 .. 1}
+//            for f < 1/2 (D(s) in {D - 1, D}), o.x + {-2 .. 0} otherwise: every sample with
+//            |delta(s) - delta(c)| < 1/2 px.
+// Samples a window misses (folding / discontinuous flow) are added with atomics.
+//
+// Three launches (one pixel per lane, a wave = 64 consecutive pixels of a row):
+//   tap   per sample: (ix, iy) into the workspace (8 B, exact fp32: every later weight is
+//         formed from them exactly as warp_tap does) and dflow.
+//   pull  per dimg pixel: the window candidates' weights from their stored taps, dimg as a
+//         plain store (no zero-fill, no atomics, a fixed summation order); and per sample
+//         (the same index) the ownership check of its 4 corners -> a far-corner byte.
+//   far   reads the far bytes (four per lane) and adds the far corners with global atomics.
+// Workspace (dvie_warp_ws_floats): taps 2*n*h*w floats, then n*h*w far bytes.
+constexpr unsigned kWarpOOB = 0x80000000u;
 
-// s*(c): c minus the integer displacement of the sample at c
-__device__ __forceinline__ int2 warp_pull_origin(const dvie_warp_desc& p, const float* fl0, const float* fl1, int cx,
-                                                 int cy) {
-  const long long fo = (long long)cy * p.w + cx;
-  const WarpTap t = warp_tap(cx, cy, fl0[fo], fl1[fo], p.w, p.h, p.align_corners);
-  return make_int2(2 * cx - t.x0, 2 * cy - t.y0);
+struct PullWin {
+  int sx0, sy0;  // first column / row of the window of samples pulled by c
+};
+
+// c's window, from the stored tap (ix, iy) of the sample AT c
+template <int WIN>
+__device__ __forceinline__ PullWin warp_win(int cx, int cy, float ix, float iy) {
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  PullWin w;
+  w.sx0 = 2 * cx - (int)fx0 + (WIN == 4 ? -2 : (ix - fx0 < 0.5f ? -1 : -2));
+  w.sy0 = 2 * cy - (int)fy0 + (WIN == 4 ? -2 : (iy - fy0 < 0.5f ? -1 : -2));
+  return w;
 }
 
-// the one ownership rule both passes apply: is sample (sx, sy) a candidate of cell c?
-__device__ __forceinline__ bool warp_pulled(int2 o, int sx, int sy) {
-  return (unsigned)(sx - o.x - WP_LO) <= (unsigned)(WP_HI - WP_LO) &&
-         (unsigned)(sy - o.y - WP_LO) <= (unsigned)(WP_HI - WP_LO);
+template <int WIN>
+__device__ __forceinline__ bool warp_pulled(const PullWin& w, int sx, int sy) {
+  return (unsigned)(sx - w.sx0) <= (unsigned)(WIN - 1) && (unsigned)(sy - w.sy0) <= (unsigned)(WIN - 1);
 }
 
-// a wave covers 256 consecutive dimg pixels of one row (4 per lane, 64 apart)
-__global__ __launch_bounds__(256) void warp_bwd_pull_kernel(const dvie_warp_desc p) {
-  const int segs = (p.w + 255) >> 8;
-  const int waves = p.n * p.h * segs;
+__device__ __forceinline__ float2 warp_ld_tap(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+
+__device__ __forceinline__ unsigned char* warp_far_bytes(const dvie_warp_desc& p) {
+  return (unsigned char*)(p.ws + ((2LL * p.n * p.h * p.w + 3) & ~3LL));  // 16-B aligned
+}
+
+// wave -> (image, row, 64-pixel segment); lane -> column
+struct WarpRow {
+  int n, y, x;
+};
+__device__ __forceinline__ WarpRow warp_row(const dvie_warp_desc& p, int wv, int lane) {
+  const int segs = (p.w + 63) >> 6;
+  const int sg = wv % segs, r = wv / segs;
+  WarpRow q;
+  q.y = r % p.h;
+  q.n = r / p.h;
+  q.x = (sg << 6) + lane;
+  return q;
+}
+
+// tap pass
+template <int CC>
+__global__ __launch_bounds__(256) void warp_bwd_tap_kernel(const dvie_warp_desc p) {
+  const int waves = p.n * p.h * ((p.w + 63) >> 6);
   const int lane = threadIdx.x & 63;
   const long long hw = (long long)p.h * p.w;
   for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
        wv += gridDim.x * 4) {
-    const int sg = wv % segs;
-    const int r = wv / segs;
-    const int cy = r % p.h, n = r / p.h;
-    const float* fl0 = p.flow + (long long)n * 2 * hw;
-    const float* fl1 = fl0 + hw;
-    const __amdgpu_buffer_rsrc_t rf0 = warp_plane(fl0, hw), rf1 = warp_plane(fl1, hw);
-#pragma unroll 1
-    for (int k = 0; k < 4; ++k) {
-      const int cx = (sg << 8) + lane + 64 * k;
-      if (cx >= p.w) continue;
-      const int2 o = warp_pull_origin(p, fl0, fl1, cx, cy);
-      // phase 1: the 16 candidates' weights for c (0 where c is not one of their corners).
-      // Buffer loads with 32-bit offsets; a candidate outside the image gets an out-of-range
-      // offset (loads return 0) and a zero weight, so every load issues unconditionally.
-      constexpr int NC = (WP_HI - WP_LO + 1) * (WP_HI - WP_LO + 1);
-      unsigned off[NC];
-      float fxs[NC], fys[NC];
+    const WarpRow q = warp_row(p, wv, lane);
+    if (q.x >= p.w) continue;
+    const int n = q.n;
+    const long long fo = (long long)q.y * p.w + q.x;
+    const WarpTap t = warp_tap(q.x, q.y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo],
+                               p.w, p.h, p.align_corners);
+    if (p.dflow) {
+      const bool pair = __all(t.vx0 && t.vx1);
+      float gix = 0.f, giy = 0.f;
+      if constexpr (CC > 0) {
+        float v[CC][4], go[CC];
 #pragma unroll
-      for (int q = 0; q < NC; ++q) {
-        const int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
-        const bool in = (unsigned)sx < (unsigned)p.w && (unsigned)sy < (unsigned)p.h;
-        off[q] = in ? (unsigned)(sy * p.w + sx) * 4u : 0x80000000u;
-        fxs[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf0, off[q], 0, 0));
-        fys[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf1, off[q], 0, 0));
+        for (int c = 0; c < CC; ++c) {
+          const long long base = ((long long)n * CC + c) * hw;
+          warp_corners(warp_plane(p.img + base, hw), t, p.w, v[c][0], v[c][1], v[c][2], v[c][3], pair);
+          go[c] = p.dout[base + fo];
+        }
+#pragma unroll
+        for (int c = 0; c < CC; ++c) warp_dflow_terms(v[c][0], v[c][1], v[c][2], v[c][3], go[c], t, gix, giy);
+      } else {
+        for (int c = 0; c < p.c; ++c) {
+          const long long base = ((long long)n * p.c + c) * hw;
+          float a, b, cc, dd;
+          warp_corners(warp_plane(p.img + base, hw), t, p.w, a, b, cc, dd, pair);
+          warp_dflow_terms(a, b, cc, dd, p.dout[base + fo], t, gix, giy);
+        }
       }
-      float wq[NC];
-#pragma unroll
-      for (int q = 0; q < NC; ++q) {
-        const int sx = o.x + WP_LO + q % (WP_HI - WP_LO + 1), sy = o.y + WP_LO + q / (WP_HI - WP_LO + 1);
-        const float ix = unnorm(linspace_pm1(sx, p.w) - fxs[q], p.w, p.align_corners);
-        const float iy = unnorm(linspace_pm1(sy, p.h) - fys[q], p.h, p.align_corners);
-        const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
-        const int qx = cx - x0, qy = cy - y0;  // 0/1: c is the x0/x1, y0/y1 corner of s
-        // the bilinear weight exactly as warp_tap forms it (wnw / wne / wsw / wse)
-        const float w = (qx == 0 ? (float)(x0 + 1) - ix : ix - (float)x0) *
-                        (qy == 0 ? (float)(y0 + 1) - iy : iy - (float)y0);
-        wq[q] = (off[q] != 0x80000000u && (unsigned)qx <= 1u && (unsigned)qy <= 1u) ? w : 0.f;
-      }
-      // phase 2: dimg[c] = sum over candidates of weight * dout[s], in candidate order
-      // (a zero weight adds +0: the candidate did not hit c)
-      for (int ch = 0; ch < p.c; ++ch) {
-        const long long plane = ((long long)n * p.c + ch) * hw;
-        const __amdgpu_buffer_rsrc_t rg = warp_plane(p.dout + plane, hw);
-        float g[NC];
-#pragma unroll
-        for (int q = 0; q < NC; ++q) g[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, off[q], 0, 0));
-        float acc = 0.f;
-#pragma unroll
-        for (int q = 0; q < NC; ++q) acc += wq[q] * g[q];
-        p.dimg[plane + (long long)cy * p.w + cx] = acc;
-      }
+      const float sx = p.align_corners ? (float)(p.w - 1) / 2.f : (float)p.w / 2.f;
+      const float sy = p.align_corners ? (float)(p.h - 1) / 2.f : (float)p.h / 2.f;
+      p.dflow[((long long)n * 2 + 0) * hw + fo] = -gix * sx;
+      p.dflow[((long long)n * 2 + 1) * hw + fo] = -giy * sy;
     }
+    if (p.dimg) *(float2*)(p.ws + 2 * ((long long)n * hw + fo)) = make_float2(t.ix, t.iy);
   }
 }
 
-// dflow for every sample and, with dimg, the (sample, corner) pairs the pull pass misses
-// (global atomics, launched after it).  A wave covers 256 consecutive pixels of a row (4 per
-// lane, 64 apart), so the image planes are wave-uniform buffer resources.
-__global__ __launch_bounds__(256) void warp_bwd_flow_kernel(const dvie_warp_desc p) {
-  const int segs = (p.w + 255) >> 8;
-  const int waves = p.n * p.h * segs;
+// pull pass
+template <int WIN, int CC>
+__global__ __launch_bounds__(256) void warp_bwd_pull_kernel(const dvie_warp_desc p) {
+  constexpr int NC = WIN * WIN;
+  const int waves = p.n * p.h * ((p.w + 63) >> 6);
   const int lane = threadIdx.x & 63;
   const long long hw = (long long)p.h * p.w;
   for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
        wv += gridDim.x * 4) {
-    const int sg = wv % segs;
-    const int r = wv / segs;
-    const int y = r % p.h, n = r / p.h;
-#pragma unroll 1
-    for (int k = 0; k < 4; ++k) {
-      const int x = (sg << 8) + lane + 64 * k;
-      const bool live = x < p.w;
-      const int xl = live ? x : p.w - 1;
-      const long long fo = (long long)y * p.w + xl;
-      const WarpTap t = warp_tap(xl, y, p.flow[(long long)n * 2 * hw + fo], p.flow[((long long)n * 2 + 1) * hw + fo],
-                                 p.w, p.h, p.align_corners);
-      // (sample, corner) pairs the pull pass misses (evaluated once, shared by all channels)
-      bool far[4] = {false, false, false, false};
-      if (p.dimg && live) {
-        const float* fl0 = p.flow + (long long)n * 2 * hw;
-        const int cxs[4] = {t.x0, t.x0 + 1, t.x0, t.x0 + 1}, cys[4] = {t.y0, t.y0, t.y0 + 1, t.y0 + 1};
-        const bool val[4] = {t.vy0 && t.vx0, t.vy0 && t.vx1, t.vy1 && t.vx0, t.vy1 && t.vx1};
+    const WarpRow rq = warp_row(p, wv, lane);
+    const int n = rq.n, cx = rq.x, cy = rq.y;
+    if (cx >= p.w) continue;
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc(p.ws + 2 * (long long)n * hw, 0, (int)(hw * 8), 0x00020000);
+    const float2 tc = warp_ld_tap(rt, (unsigned)(cy * p.w + cx) * 8u);
+    // round trip 2: the candidates' taps, their dout values (every channel), and the taps of
+    // the corners of the sample AT c (for the ownership check), all issued together
+    const int x0 = (int)floorf(tc.x), y0 = (int)floorf(tc.y);
+    const PullWin win = warp_win<WIN>(cx, cy, tc.x, tc.y);
+    // candidate offsets: the window's rows and columns are checked once (separable)
+    int rowo[WIN];
+    bool rowok[WIN], colok[WIN];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (val[q]) far[q] = !warp_pulled(warp_pull_origin(p, fl0, fl0 + hw, cxs[q], cys[q]), xl, y);
-      }
-      const bool any_far = far[0] || far[1] || far[2] || far[3];
-      float gix = 0.f, giy = 0.f;
-      for (int c = 0; c < p.c; ++c) {
-        const long long base = ((long long)n * p.c + c) * hw;
-        float a, b, cc, dd;
-        warp_corners(warp_plane(p.img + base, hw), t, p.w, a, b, cc, dd);
-        const float go = p.dout[base + fo];
-        warp_bwd_pixel(a, b, cc, dd, go, t, gix, giy, [](int, int, float) {});
-        if (any_far) {
-          if (far[0]) atomicAdd(p.dimg + base + (long long)t.y0 * p.w + t.x0, t.wnw * go);
-          if (far[1]) atomicAdd(p.dimg + base + (long long)t.y0 * p.w + t.x0 + 1, t.wne * go);
-          if (far[2]) atomicAdd(p.dimg + base + (long long)(t.y0 + 1) * p.w + t.x0, t.wsw * go);
-          if (far[3]) atomicAdd(p.dimg + base + (long long)(t.y0 + 1) * p.w + t.x0 + 1, t.wse * go);
+    for (int j = 0; j < WIN; ++j) {
+      rowok[j] = (unsigned)(win.sy0 + j) < (unsigned)p.h;
+      colok[j] = (unsigned)(win.sx0 + j) < (unsigned)p.w;
+      rowo[j] = (win.sy0 + j) * p.w + win.sx0;
+    }
+    unsigned off[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q)
+      off[q] = rowok[q / WIN] && colok[q % WIN] ? (unsigned)(rowo[q / WIN] + q % WIN) : kWarpOOB;
+    // wide: every lane's window columns lie inside the image (wave-uniform), so a window row
+    // is one contiguous run -- its taps one 16-B + one 8-B (WIN 3) or two 16-B loads, its
+    // dout values one 12-B / 16-B load per channel -- instead of one load per candidate
+    // (these gathers are bound by vector-memory instructions, not bytes)
+    const bool wide = __all(colok[0] && colok[WIN - 1]);
+    float2 tq[NC];
+    if (wide) {
+#pragma unroll
+      for (int j = 0; j < WIN; ++j) {
+        const unsigned rb = rowok[j] ? (unsigned)rowo[j] * 8u : kWarpOOB;
+        const auto a = __builtin_amdgcn_raw_buffer_load_b128(rt, rb, 0, 0);
+        tq[j * WIN] = make_float2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        tq[j * WIN + 1] = make_float2(__uint_as_float(a[2]), __uint_as_float(a[3]));
+        if constexpr (WIN == 3) {
+          tq[j * WIN + 2] = warp_ld_tap(rt, rowok[j] ? rb + 16u : kWarpOOB);
+        } else {
+          const auto b = __builtin_amdgcn_raw_buffer_load_b128(rt, rowok[j] ? rb + 16u : kWarpOOB, 0, 0);
+          tq[j * WIN + 2] = make_float2(__uint_as_float(b[0]), __uint_as_float(b[1]));
+          tq[j * WIN + 3] = make_float2(__uint_as_float(b[2]), __uint_as_float(b[3]));
         }
       }
-      if (p.dflow && live) warp_store_dflow(p, n, fo, gix, giy);
+    } else {
+#pragma unroll
+      for (int q = 0; q < NC; ++q) tq[q] = warp_ld_tap(rt, off[q] == kWarpOOB ? kWarpOOB : off[q] * 8u);
     }
+    auto load_go = [&](int ch, float* g) {
+      const __amdgpu_buffer_rsrc_t rg = warp_plane(p.dout + ((long long)n * p.c + ch) * hw, hw);
+      if (wide) {
+#pragma unroll
+        for (int j = 0; j < WIN; ++j) {
+          const unsigned rb = rowok[j] ? (unsigned)rowo[j] * 4u : kWarpOOB;
+          if constexpr (WIN == 3) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rg, rb, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) g[j * WIN + i] = __uint_as_float(v[i]);
+          } else {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rg, rb, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g[j * WIN + i] = __uint_as_float(v[i]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < NC; ++q)
+          g[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               rg, off[q] == kWarpOOB ? kWarpOOB : off[q] * 4u, 0, 0));
+      }
+    };
+    float gv[CC > 0 ? CC : 1][NC];
+    if constexpr (CC > 0) {
+#pragma unroll
+      for (int ch = 0; ch < CC; ++ch) load_go(ch, gv[ch]);
+    }
+    // the corners' taps: the two of a corner row are adjacent (one 16-B load when every
+    // lane's x0 and x0 + 1 lie inside the image)
+    float2 te[4];
+    bool ve[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ve[q] = (unsigned)(x0 + (q & 1)) < (unsigned)p.w && (unsigned)(y0 + (q >> 1)) < (unsigned)p.h;
+    if (__all(x0 >= 0 && x0 + 1 < p.w)) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const auto a = __builtin_amdgcn_raw_buffer_load_b128(rt, ve[2 * r] ? (unsigned)((y0 + r) * p.w + x0) * 8u : kWarpOOB, 0, 0);
+        te[2 * r] = make_float2(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        te[2 * r + 1] = make_float2(__uint_as_float(a[2]), __uint_as_float(a[3]));
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        te[q] = warp_ld_tap(rt, ve[q] ? (unsigned)((y0 + (q >> 1)) * p.w + x0 + (q & 1)) * 8u : kWarpOOB);
+    }
+    // the candidates' weights for c (0 where c is not one of their corners, or the candidate
+    // lies outside the image).  c is the x0 corner of s iff cx <= ix < cx + 1 and the x1
+    // corner iff cx - 1 <= ix < cx, so the factor warp_tap forms, (x0 + 1) - ix or ix - x0,
+    // is (cx + 1) - ix or ix - (cx - 1): the same fp32 operations, without floor/convert
+    const float fcx = (float)cx, fcy = (float)cy;
+    const float cxp = fcx + 1.f, cxm = fcx - 1.f, cyp = fcy + 1.f, cym = fcy - 1.f;
+    float wq[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const float ix = tq[q].x, iy = tq[q].y;
+      const float wx = ix >= fcx ? cxp - ix : ix - cxm;
+      const float wy = iy >= fcy ? cyp - iy : iy - cym;
+      const bool hit = off[q] != kWarpOOB && ix >= cxm && ix < cxp && iy >= cym && iy < cyp;
+      wq[q] = hit ? wx * wy : 0.f;
+    }
+    // dimg[c] = sum over candidates of weight * dout[s], in candidate order (a zero weight
+    // adds +0: the candidate did not hit c)
+    const long long co = (long long)cy * p.w + cx;
+    if constexpr (CC > 0) {
+#pragma unroll
+      for (int ch = 0; ch < CC; ++ch) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) acc += wq[q] * gv[ch][q];
+        p.dimg[((long long)n * CC + ch) * hw + co] = acc;
+      }
+    } else {
+      for (int ch = 0; ch < p.c; ++ch) {
+        load_go(ch, gv[0]);
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NC; ++q) acc += wq[q] * gv[0][q];
+        p.dimg[((long long)n * p.c + ch) * hw + co] = acc;
+      }
+    }
+    // ownership of the sample AT c (s = c): bit q set = corner q's window misses it
+    unsigned fb = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ex = x0 + (q & 1), ey = y0 + (q >> 1);
+      if (ve[q] && !warp_pulled<WIN>(warp_win<WIN>(ex, ey, te[q].x, te[q].y), cx, cy)) fb |= 1u << q;
+    }
+    warp_far_bytes(p)[(long long)n * hw + co] = (unsigned char)fb;
+  }
+}
+
+// far pass: four samples per lane (one 4-byte load of far bytes); every set bit adds that
+// corner with a global atomic
+__device__ __forceinline__ void warp_far_sample(const dvie_warp_desc& p, long long gs, unsigned fb, long long hw) {
+  const int n = (int)(gs / hw);
+  const long long fo = gs - (long long)n * hw;
+  // the stored tap (the weights the pull pass forms for its candidates, bit for bit)
+  const float2 tp = *(const float2*)(p.ws + 2 * gs);
+  const float ix = tp.x, iy = tp.y;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = (int)fx0, y0 = (int)fy0;
+  const float wts[4] = {((fx0 + 1.f) - ix) * ((fy0 + 1.f) - iy), (ix - fx0) * ((fy0 + 1.f) - iy),
+                        ((fx0 + 1.f) - ix) * (iy - fy0), (ix - fx0) * (iy - fy0)};
+  for (int c = 0; c < p.c; ++c) {
+    const long long base = ((long long)n * p.c + c) * hw;
+    const float go = p.dout[base + fo];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (fb & (1u << q)) atomicAdd(p.dimg + base + (long long)(y0 + (q >> 1)) * p.w + x0 + (q & 1), wts[q] * go);
+  }
+}
+
+__global__ __launch_bounds__(256) void warp_bwd_far_kernel(const dvie_warp_desc p) {
+  const long long hw = (long long)p.h * p.w;
+  const long long total = (long long)p.n * hw;
+  const unsigned char* fbytes = warp_far_bytes(p);
+  for (long long i0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < total;
+       i0 += (long long)gridDim.x * blockDim.x * 4) {
+    unsigned w4;
+    if (i0 + 4 <= total) {
+      w4 = *(const unsigned*)(fbytes + i0);
+    } else {
+      w4 = 0;
+      for (int j = 0; i0 + j < total; ++j) w4 |= (unsigned)fbytes[i0 + j] << (8 * j);
+    }
+    if (!w4) continue;
+    for (int j = 0; j < 4; ++j)
+      if ((w4 >> (8 * j)) & 15u) warp_far_sample(p, i0 + j, (w4 >> (8 * j)) & 15u, hw);
   }
 }
 
@@ -334,24 +531,55 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->out && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
   const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
   DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
-  hipLaunchKernelGGL(warp_fwd_kernel, dim3(grid_for(waves * 256)), dim3(256), 0, (hipStream_t)stream, *d);
+  const int grid = grid_for(waves * 256);
+  if (d->c == 3)
+    hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
 
-
 size_t dvie_warp_ws_floats(const dvie_warp_desc* d) {
-  (void)d;
-  return 0;  // the backward needs no workspace (kept for ABI stability)
+  if (!d || !d->dimg) return 0;  // dflow only: no workspace
+  const size_t px = (size_t)d->n * d->h * d->w;
+  return (2 * px + 3) / 4 * 4 + (px + 15) / 16 * 4;  // taps, far bytes (16-B aligned)
 }
+
+// pull window width (see warp_bwd_pull_kernel): 4 by default -- a noisy flow (a flow net early
+// in training) stays off the atomic path; DVIE_WARP_WIN=3 for A/B runs (15% faster on a
+// smooth flow, 22% slower with 0.2 px per-pixel noise at 1024x2048: profiles/r02_warp/)
+static const int warp_win_env = getenv("DVIE_WARP_WIN") && atoi(getenv("DVIE_WARP_WIN")) == 3 ? 3 : 4;
 
 int dvie_warp_bwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->dout && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
-  DVIE_CHECK_ARG((long long)d->h * d->w < (1LL << 29), "warp: size");
+  DVIE_CHECK_ARG((long long)d->h * d->w < (1LL << 28), "warp: size");  // tap offsets: 8 B/px
+  DVIE_CHECK_ARG((long long)d->n * d->h * d->w < (1LL << 31), "warp: size");
+  DVIE_CHECK_ARG(!d->dimg || d->ws, "warp: dimg needs the workspace (dvie_warp_ws_floats)");
   hipStream_t s = (hipStream_t)stream;
-  const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
+  const long long waves = (long long)d->n * d->h * ((d->w + 63) / 64);
   DVIE_CHECK_ARG(waves < (1LL << 31), "warp: size");
-  if (d->dimg) hipLaunchKernelGGL(warp_bwd_pull_kernel, dim3(grid_for(waves * 256)), dim3(256), 0, s, *d);
-  hipLaunchKernelGGL(warp_bwd_flow_kernel, dim3(grid_for(waves * 256)), dim3(256), 0, s, *d);
+  if (!d->dimg && !d->dflow) return DVIE_OK;
+  const int grid = (int)std::min<long long>((waves + 3) / 4, 16384);
+  const bool c3 = d->c == 3;
+  if (c3)
+    hipLaunchKernelGGL(warp_bwd_tap_kernel<3>, dim3(grid), dim3(256), 0, s, *d);
+  else
+    hipLaunchKernelGGL(warp_bwd_tap_kernel<0>, dim3(grid), dim3(256), 0, s, *d);
+  if (d->dimg) {
+    if (warp_win_env == 3) {
+      if (c3)
+        hipLaunchKernelGGL((warp_bwd_pull_kernel<3, 3>), dim3(grid), dim3(256), 0, s, *d);
+      else
+        hipLaunchKernelGGL((warp_bwd_pull_kernel<3, 0>), dim3(grid), dim3(256), 0, s, *d);
+    } else {
+      if (c3)
+        hipLaunchKernelGGL((warp_bwd_pull_kernel<4, 3>), dim3(grid), dim3(256), 0, s, *d);
+      else
+        hipLaunchKernelGGL((warp_bwd_pull_kernel<4, 0>), dim3(grid), dim3(256), 0, s, *d);
+    }
+    const long long quads = ((long long)d->n * d->h * d->w + 3) / 4;
+    hipLaunchKernelGGL(warp_bwd_far_kernel, dim3((unsigned)std::min<long long>((quads + 255) / 256, 4096)), dim3(256), 0, s, *d);
+  }
   DVIE_RETURN_LAUNCH();
 }
 

@@ -42,7 +42,11 @@ class _WarpFn(torch.autograd.Function):
         d.dimg = dx.data_ptr() if dx is not None else None
         d.dflow = dflow.data_ptr() if dflow is not None else None
         d.n, d.c, d.h, d.w, d.align_corners = n, c, h, w, int(ctx.ac)
-        L.check(L.load().dvie_warp_bwd(ctypes.byref(d), L.stream_ptr(x.device)), "warp bwd")
+        lib = L.load()
+        nws = lib.dvie_warp_ws_floats(ctypes.byref(d))
+        ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x.device)
+        d.ws = ws.data_ptr()
+        L.check(lib.dvie_warp_bwd(ctypes.byref(d), L.stream_ptr(x.device)), "warp bwd")
         return dx, dflow, None
 
 

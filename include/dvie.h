@@ -286,11 +286,12 @@ size_t dvie_loss_ws_floats(const dvie_loss_desc* d);
  * zeros padding, align_corners=True as in the pinned torch 1.0.1):
  *   gx = linspace(-1,1,W)[x] - flow[n,0,y,x],  gy = linspace(-1,1,H)[y] - flow[n,1,y,x]
  *   out[n,c,y,x] = bilinear(img[n,c], (gx+1)/2*(W-1), (gy+1)/2*(H-1))
- * fp32, NCHW contiguous.  Backward: dimg and dflow (both overwritten), given dout.  dimg
- * is produced by ownership: one workgroup per 64x16 tile of dimg sums, in LDS, the corners
- * of the samples in its flow-displaced window and stores the tile; a second pass computes
- * dflow and adds the few corners no window owns (large or discontinuous flow) with global
- * atomics.  dimg = NULL computes dflow only.  `ws` is reserved (dvie_warp_ws_floats = 0).
+ * fp32, NCHW contiguous.  Backward: dimg and dflow (both overwritten), given dout.  Three
+ * launches: per sample its source position (ix, iy) into `ws` and dflow; per dimg pixel the
+ * samples of a 3x3 window around c minus its displacement (the side chosen by the fractional
+ * part) gathered as a plain store, plus the per-sample check that appends samples a corner's
+ * window misses to a far list in `ws`; global atomics for the listed samples.  dimg = NULL
+ * computes dflow only (ws may be NULL).  `ws` holds dvie_warp_ws_floats(d) floats.
  */
 typedef struct dvie_warp_desc {
   const float* img;

@@ -146,12 +146,15 @@ def test_warp(dev):
 
 
 @pytest.mark.parametrize("with_dimg", [True, False])
-@pytest.mark.parametrize("shape", [(2, 5, 40, 136), (1, 3, 33, 66)])
-def test_warp_multi_tile(dev, with_dimg, shape):
-    """dvie_warp_bwd through the C ABI on frames spanning many 64x16 tiles: a smooth flow of
-    a few pixels (samples that cross tile borders but stay in the LDS region) plus a sparse
-    set of large displacements (the far-sample atomics); the tiled image-gradient kernel and
-    the dflow-only kernel (dimg = NULL); 5 channels exercise the partial channel block.
+@pytest.mark.parametrize("shape,far_frac", [((2, 5, 40, 136), 0.05), ((1, 3, 33, 66), 0.05), ((2, 3, 70, 200), 0.0),
+                                            ((1, 4, 37, 130), 0.002)])
+def test_warp_multi_tile(dev, with_dimg, shape, far_frac):
+    """dvie_warp_bwd through the C ABI on frames spanning many 256-pixel row segments: a
+    smooth flow of a few pixels (every sample inside its corners' 3x3 pull windows) plus a
+    sparse set of large displacements (far corners and their atomics; a tile holding one
+    reads from global memory, a tile without from its LDS-staged region: far_frac 0 and
+    0.002 keep most tiles on the LDS path); the dimg + dflow path and the dflow-only path
+    (dimg = NULL, no workspace); 3-5 channels.
     Tolerances: out 1e-5, dimg 1e-4, dflow 1e-3 abs."""
     import ctypes
     from deep_video_interpolation_extrapolation_amd import _lib as L
@@ -161,7 +164,7 @@ def test_warp_multi_tile(dev, with_dimg, shape):
     yy, xx = torch.meshgrid(torch.arange(h, dtype=torch.float32), torch.arange(w, dtype=torch.float32), indexing="ij")
     flow = torch.stack([torch.sin(xx / 9.0 + yy / 13.0) * 6.0 / w, torch.cos(yy / 7.0 - xx / 17.0) * 5.0 / h])
     flow = flow.unsqueeze(0).repeat(n, 1, 1, 1) + (torch.rand((n, 2, h, w), generator=g) - 0.5) * 0.02
-    far = torch.rand((n, 1, h, w), generator=g) < 0.05
+    far = torch.rand((n, 1, h, w), generator=g) < far_frac
     flow = torch.where(far, (torch.rand((n, 2, h, w), generator=g) * 2 - 1) * 0.8, flow)
     dout = torch.randn((n, c, h, w), generator=g)
     xr, fr = x.clone().requires_grad_(True), flow.clone().requires_grad_(True)
@@ -177,6 +180,8 @@ def test_warp_multi_tile(dev, with_dimg, shape):
     d.n, d.c, d.h, d.w, d.align_corners = n, c, h, w, 1
     if not with_dimg:
         d.dimg = None
+    ws = torch.full((max(lib.dvie_warp_ws_floats(ctypes.byref(d)), 1),), float("nan"), device=dev)
+    d.ws = ws.data_ptr()
     s = L.stream_ptr(dev)
     L.check(lib.dvie_warp_fwd(ctypes.byref(d), s), "warp fwd")
     L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), "warp bwd")

@@ -48,7 +48,8 @@ def main(d):
         if k not in dur:
             continue
         calls, avg_ns = dur[k]
-        n_pmc = max(1, len({x for x in launches[k]}) // 4)  # each launch appears in every pass
+        n_pass = len(glob.glob(f"{d}/p[0-9]*/"))
+        n_pmc = max(1, len({x for x in launches[k]}) // max(1, n_pass))  # each launch appears in every pass
         grbm = c.get("GRBM_GUI_ACTIVE", 0.0)
         util = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * grbm / 8.0) if grbm else 0.0
         hbm = (2.0 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024.0 / n_pmc
@@ -63,6 +64,15 @@ def main(d):
     for _, k, calls, us, util, mb, gbs, wa, wi, ac, wl, bc in rows:
         print(f"{k[:48]:48s} {calls:5d} {us:8.1f} {100 * util:6.1f} {mb:8.1f} {gbs:7.0f} {wa:5.2f} {wi:5.2f} "
               f"{ac:5.2f} {wl:5.2f} {bc:8.3f}")
+    print()
+    print(f"{'kernel (instructions per wave)':48s} {'waves':>9s} {'VALU':>8s} {'VMEM_RD':>8s} {'VMEM_WR':>8s} {'LDS':>8s} "
+          f"{'SALU':>8s}")
+    for _, k, *_ in rows:
+        c = tot[k]
+        wv = c.get("SQ_WAVES", 0.0) or 1.0
+        print(f"{k[:48]:48s} {wv:9.0f} {c.get('SQ_INSTS_VALU', 0) / wv:8.1f} {c.get('SQ_INSTS_VMEM_RD', 0) / wv:8.1f} "
+              f"{c.get('SQ_INSTS_VMEM_WR', 0) / wv:8.1f} {c.get('SQ_INSTS_LDS', 0) / wv:8.1f} "
+              f"{c.get('SQ_INSTS_SALU', 0) / wv:8.1f}")
 
 
 if __name__ == "__main__":

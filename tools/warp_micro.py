@@ -27,16 +27,20 @@ def setup(dev, n, c, H, W):
     d = L.WarpDesc()
     d.img, d.flow, d.out, d.dout, d.dimg, d.dflow = (t.data_ptr() for t in (x, flow, out, go, dx, dflow))
     d.n, d.c, d.h, d.w, d.align_corners = n, c, H, W, 1
-    return lib, d, (x, flow, go, out, dx, dflow)
+    ws = torch.empty(lib.dvie_warp_ws_floats(ctypes.byref(d)), device=dev)
+    d.ws = ws.data_ptr()
+    return lib, d, (x, flow, go, out, dx, dflow, ws)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--shape", default=None, help="one n,c,H,W shape instead of the two defaults")
     a = ap.parse_args()
+    shapes = [tuple(map(int, a.shape.split(",")))] if a.shape else [(8, 3, 256, 512), (8, 3, 1024, 2048)]
     dev = torch.device("cuda:0")
     s = L.stream_ptr(dev)
-    for (n, c, H, W) in ((8, 3, 256, 512), (8, 3, 1024, 2048)):
+    for (n, c, H, W) in shapes:
         lib, d, keep = setup(dev, n, c, H, W)
         dx = keep[4]
         for tag in ("fwd", "bwd", "bwd_dflow_only"):
@@ -46,7 +50,7 @@ def main():
                 if tag == "fwd":
                     L.check(lib.dvie_warp_fwd(ctypes.byref(d), s), tag)
                 else:
-                                L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), tag)
+                    L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), tag)
             for _ in range(3):
                 run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
