@@ -281,6 +281,119 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
   }
 }
 
+// 1x1 weight gradient of two wide layers (c, cout > 128; the 448 -> 448 HRNet heads): a
+// workgroup owns a 256 x 256 (co x ci) block, so each 64-pixel tile's G and X images (32 KB
+// each) feed 4x the MFMAs of the 128 x 128 block (half the L2 -> CU bytes per MFMA: the
+// 128-block kernel sat at the CU's fetch rate).  1x1 stride-1 unpadded: the pixels are one
+// flat range, a tile is 64 consecutive pixels.  8 waves = 2 (co) x 4 (ci), a wave owns
+// 128 co x 64 ci (4 x 2 accumulators); G and X are double-buffered (128 KB), one barrier per
+// tile.  One partial slab per split, summed by dvie_wgrad_reduce.
+__global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
+                                                         int n_tiles) {
+  constexpr int NW = 8, NSUB = 4, SUB = 64 * 128, TSZ = NSUB * SUB;
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TSZ];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned OOB = 0xFFFFFFF0u;
+  const int npair = n_co * n_ci;
+  const int lid = xcd_chunk(blockIdx.x, gridDim.x);
+  const int pair = lid % npair, split = lid / npair;
+  const int c0 = (pair % n_co) * 256, k0 = (pair / n_co) * 256;
+  const int t_begin = (int)((long long)split * n_tiles / splits);
+  const int t_end = (int)((long long)(split + 1) * n_tiles / splits);
+  const long long npix = (long long)p.n * p.oh * p.ow;
+  const unsigned long long gbytes = ((unsigned long long)npix - 1) * (unsigned long long)p.g_ld * 2ull + (unsigned long long)p.cout * 2ull;
+  const unsigned long long xbytes = ((unsigned long long)npix - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)p.g + (size_t)c0 * 2), 0, (int)(gbytes - (unsigned long long)c0 * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const char*)p.x + (size_t)k0 * 2), 0, (int)(xbytes - (unsigned long long)k0 * 2), 0x00020000);
+  const unsigned grow = (unsigned)p.g_ld * 2u, xrow = (unsigned)p.x_ld * 2u;
+  // DMA lane geometry as in wgrad_halo_kernel: piece = 8 pixels x 128 B
+  const int lrow = lane >> 3, lch = lane & 7;
+  const int lcs = lch ^ (((lrow >> 1) & 1) << 2);
+  auto issue = [&](int tile, int buf) {
+#pragma unroll
+    for (int q = 0; q < NSUB * 8 / NW; ++q) {
+      const int pc = wave + NW * q, sub = pc >> 3, pr = pc & 7;
+      const long long P = (long long)tile * 64 + pr * 8 + lrow;
+      const int ch = 64 * sub + lcs * 8;
+      const unsigned og = P < npix && c0 + ch < p.cout ? (unsigned)P * grow + (unsigned)ch * 2u : OOB;
+      const unsigned ox = P < npix && k0 + ch < p.c ? (unsigned)P * xrow + (unsigned)ch * 2u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_ptr_wg)(smem + buf * TSZ + sub * SUB + pr * 1024), 16, og, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_wg)(smem + (2 + buf) * TSZ + sub * SUB + pr * 1024), 16, ox,
+                                               0, 0, 0);
+    }
+  };
+  const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  auto tr_off = [&](int col0) {
+    const int col = col0 + 16 * (grp & 1) + 4 * tp;
+    const int ch = (col >> 3) ^ (((tq >> 1) & 1) << 2);
+    return tq * 128 + ch * 16 + (col & 7) * 2 + 8 * 128 * (grp >> 1);
+  };
+  const int wco = wave >> 2, wci = wave & 3;
+  int g_off[4], x_off[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = wco * 128 + 32 * j;
+    g_off[j] = (col >> 6) * SUB + tr_off(col & 63);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int col = wci * 64 + 32 * i;
+    x_off[i] = (col >> 6) * SUB + tr_off(col & 63);
+  }
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+  if (t_begin < t_end) {
+    issue(t_begin, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  int buf = 0;
+  for (int tile = t_begin; tile < t_end; ++tile, buf ^= 1) {
+    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+    const char* G = smem + buf * TSZ;
+    const char* X = smem + (2 + buf) * TSZ;
+#pragma unroll
+    for (int kx = 0; kx < 4; ++kx) {
+      const int r = kx * 16 * 128;
+      bf16x8 a[4], b[2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = tr_pair(G + g_off[j] + r, G + g_off[j] + r + 4 * 128);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) b[i] = tr_pair(X + x_off[i] + r, X + x_off[i] + r + 4 * 128);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[j], b[i], acc[j][i], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  // partial slab ws[split][co][ci]; C layout: column (ci) = lane & 31, rows (co) =
+  // 8*(e>>2) + 4*(lane>>5) + (e&3)
+  const int r32 = lane & 31, hh = lane >> 5;
+  float* slab = p.ws + (long long)split * p.cout * p.c;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ci = k0 + wci * 64 + 32 * i + r32;
+      if (ci >= p.c) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = c0 + wco * 128 + 32 * j + 8 * (e >> 2) + 4 * hh + (e & 3);
+        if (co < p.cout) slab[(long long)co * p.c + ci] = acc[j][i][e];
+      }
+    }
+}
+
 // diagnostic override, read once (plan-time slab counts and launches must agree):
 // DVIE_WGRAD_HALO=0 = per-tap kernel only
 static const bool wg_halo_env_off = getenv("DVIE_WGRAD_HALO") && *getenv("DVIE_WGRAD_HALO") == '0';
@@ -303,18 +416,30 @@ static bool wgrad_halo_eligible(const dvie_wgrad_desc& p) {
 }
 
 struct WgPlan {
-  int pr, tmo, tmi;
+  int pr, tmo, tmi, wide;
 };
 
+// DVIE_WG_WIDE=0: 1x1 wide layers on the 128 x 128 block kernel (A/B runs)
+static const bool wg_wide_env_off = getenv("DVIE_WG_WIDE") && *getenv("DVIE_WG_WIDE") == '0';
+
 static WgPlan wgrad_plan(const dvie_wgrad_desc& p) {
-  if (p.th == 3) return {4, 1, 1};
+  if (p.th == 3) return {4, 1, 1, 0};
+  if (!wg_wide_env_off && p.c > 128 && p.cout > 128 && p.dy0 == 0 && p.dx0 == 0 && p.oh == p.ih && p.ow == p.iw)
+    return {1, 4, 4, 1};
   const char* e = getenv("DVIE_WG_TM");  // tuning override for 1x1: "<tmo><tmi>", e.g. "11"
-  if (e && e[0] && e[1]) return {2, e[0] == '2' ? 2 : 1, e[1] == '2' ? 2 : 1};
-  return {2, p.cout > 64 ? 2 : 1, p.c > 64 ? 2 : 1};
+  if (e && e[0] && e[1]) return {2, e[0] == '2' ? 2 : 1, e[1] == '2' ? 2 : 1, 0};
+  return {2, p.cout > 64 ? 2 : 1, p.c > 64 ? 2 : 1, 0};
 }
 
 static void wgrad_tiles(const dvie_wgrad_desc& p, const WgPlan& w, int& tiles_x, int& tiles_y, int& n_tiles, int& n_co,
                         int& n_ci) {
+  if (w.wide) {  // flat 64-pixel tiles, 256-channel blocks
+    tiles_x = tiles_y = 1;
+    n_tiles = (int)(((long long)p.n * p.oh * p.ow + 63) / 64);
+    n_co = (p.cout + 255) / 256;
+    n_ci = (p.c + 255) / 256;
+    return;
+  }
   tiles_x = (p.ow + 63) / 64;
   tiles_y = (p.oh + w.pr - 1) / w.pr;
   n_tiles = tiles_x * tiles_y * p.n;
@@ -339,7 +464,9 @@ int wgrad_halo_splits(const dvie_wgrad_desc& p) {
 // DVIE_WG_MERGE=0: two slabs per split, row halves unmerged (A/B runs)
 static const int wg_merge = getenv("DVIE_WG_MERGE") && *getenv("DVIE_WG_MERGE") == '0' ? 0 : 1;
 
-int wgrad_halo_slabs(const dvie_wgrad_desc& p) { return wgrad_halo_eligible(p) && !wg_merge ? 2 * p.splits : p.splits; }
+int wgrad_halo_slabs(const dvie_wgrad_desc& p) {
+  return wgrad_halo_eligible(p) && !wg_merge && !wgrad_plan(p).wide ? 2 * p.splits : p.splits;
+}
 
 bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   if (!wgrad_halo_eligible(p)) return false;
@@ -347,6 +474,10 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   int tiles_x, tiles_y, n_tiles, n_co, n_ci;
   wgrad_tiles(p, w, tiles_x, tiles_y, n_tiles, n_co, n_ci);
   const int grid = n_co * n_ci * p.splits;
+  if (w.wide) {
+    hipLaunchKernelGGL(wgrad_wide_kernel, dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, n_tiles);
+    return true;
+  }
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
   hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
                      tiles_x, tiles_y, n_tiles, wg_merge)
