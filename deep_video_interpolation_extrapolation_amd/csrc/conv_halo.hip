@@ -508,6 +508,106 @@ static int env_cfg() {
   return e && *e ? atoi(e) : -3;
 }
 
+// Epilogue of one 32-channel x 32-pixel accumulator block (v_mfma_f32_32x32x16 layout):
+// permlane32_swap pairs the half-waves so that each lane owns 8 consecutive channels of one
+// pixel, then bias / residual / accumulate / activation / activation-derivative and one
+// 16-byte (bf16) or 2x16-byte (fp32) store per lane.  co8 = the lane's first channel of
+// pair 0 (32-block base + 8 * half); pair P adds 16.
+template <bool OUTF32>
+__device__ __forceinline__ void ws_epilogue(const dvie_conv_desc& p, const f32x16& acc, int n, int oy, int ox, int co8) {
+  float v[2][8];
+#pragma unroll
+  for (int P = 0; P < 2; ++P)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[8 * P + e]), __float_as_uint(acc[8 * P + 4 + e]),
+                                                       false, false);
+      v[P][e] = __uint_as_float(sw[0]);
+      v[P][4 + e] = __uint_as_float(sw[1]);
+    }
+  if (oy >= p.oh || ox >= p.ow) return;
+  const long long pix = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+#pragma unroll
+  for (int P = 0; P < 2; ++P) {
+    const int co = co8 + 16 * P;
+    if (co >= p.cout) continue;
+    float* w = v[P];
+    if (p.bias) {
+      const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w[e] += b0[e];
+        w[4 + e] += b1[e];
+      }
+    }
+    float t8[8];
+    if constexpr (OUTF32) {
+      float* dst = (float*)p.y + pix * p.y_ld + co;
+      if (p.res) {
+        const float* rs = (const float*)p.res + pix * p.res_ld + co;
+        const f32x4 r0 = *(const f32x4*)rs, r1 = *(const f32x4*)(rs + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[e] += r0[e];
+          w[4 + e] += r1[e];
+        }
+      }
+      if (p.beta) {
+        const f32x4 r0 = *(const f32x4*)dst, r1 = *(const f32x4*)(dst + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[e] += r0[e];
+          w[4 + e] += r1[e];
+        }
+      }
+      act_apply(w, 8, p.act, p.alpha);
+      if (p.dact) {
+        const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          t8[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
+          t8[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
+        }
+        dact_apply(w, t8, 8, p.dact, p.alpha);
+      }
+      *(f32x4*)dst = f32x4{w[0], w[1], w[2], w[3]};
+      *(f32x4*)(dst + 4) = f32x4{w[4], w[5], w[6], w[7]};
+    } else {
+      bf16_t* dst = (bf16_t*)p.y + pix * p.y_ld + co;
+      if (p.res) {
+        const i32x4 tr = *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+          w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+        }
+      }
+      if (p.beta) {
+        const i32x4 tr = *(const i32x4*)dst;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+          w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+        }
+      }
+      act_apply(w, 8, p.act, p.alpha);
+      if (p.dact) {
+        const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          t8[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
+          t8[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
+        }
+        dact_apply(w, t8, 8, p.dact, p.alpha);
+      }
+      i32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
+      *(i32x4*)dst = o;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Weight-stationary variant for single-chunk 3x3 convs (c <= 64, cout <= 64: the 64-channel
 // full-resolution HRNet branch, its data gradient, VGG conv1_2): every wave keeps the
@@ -635,98 +735,8 @@ __global__ __launch_bounds__(2 * WP * 64, 4 / WP) void conv_ws_kernel(const dvie
     // ---- epilogue straight from the accumulators (as conv_halo_kernel) ----
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      float v[2][8];
-#pragma unroll
-      for (int P = 0; P < 2; ++P)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[b][8 * P + e]),
-                                                           __float_as_uint(acc[b][8 * P + 4 + e]), false, false);
-          v[P][e] = __uint_as_float(sw[0]);
-          v[P][4 + e] = __uint_as_float(sw[1]);
-        }
       const int oy = cur.y0 + wp, ox = cur.x0 + 32 * b + r32;
-      if (oy >= p.oh || ox >= p.ow) continue;
-      const long long pix = ((long long)cur.n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
-#pragma unroll
-      for (int P = 0; P < 2; ++P) {
-        const int co = 32 * wc + 16 * P + 8 * hh;
-        if (co >= p.cout) continue;
-        float* w = v[P];
-        if (p.bias) {
-          const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            w[e] += b0[e];
-            w[4 + e] += b1[e];
-          }
-        }
-        float t8[8];
-        if constexpr (OUTF32) {
-          float* dst = (float*)p.y + pix * p.y_ld + co;
-          if (p.res) {
-            const float* rs = (const float*)p.res + pix * p.res_ld + co;
-            const f32x4 r0 = *(const f32x4*)rs, r1 = *(const f32x4*)(rs + 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              w[e] += r0[e];
-              w[4 + e] += r1[e];
-            }
-          }
-          if (p.beta) {
-            const f32x4 r0 = *(const f32x4*)dst, r1 = *(const f32x4*)(dst + 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              w[e] += r0[e];
-              w[4 + e] += r1[e];
-            }
-          }
-          act_apply(w, 8, p.act, p.alpha);
-          if (p.dact) {
-            const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              t8[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
-              t8[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
-            }
-            dact_apply(w, t8, 8, p.dact, p.alpha);
-          }
-          *(f32x4*)dst = f32x4{w[0], w[1], w[2], w[3]};
-          *(f32x4*)(dst + 4) = f32x4{w[4], w[5], w[6], w[7]};
-        } else {
-          bf16_t* dst = (bf16_t*)p.y + pix * p.y_ld + co;
-          if (p.res) {
-            const i32x4 tr = *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
-              w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
-            }
-          }
-          if (p.beta) {
-            const i32x4 tr = *(const i32x4*)dst;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
-              w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
-            }
-          }
-          act_apply(w, 8, p.act, p.alpha);
-          if (p.dact) {
-            const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              t8[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
-              t8[2 * e + 1] = __uint_as_float(((uint32_t)tz[e]) & 0xffff0000u);
-            }
-            dact_apply(w, t8, 8, p.dact, p.alpha);
-          }
-          i32x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
-          *(i32x4*)dst = o;
-        }
-      }
+      ws_epilogue<OUTF32>(p, acc[b], cur.n, oy, ox, 32 * wc + 8 * hh);
     }
     cur = nxt;
   }
@@ -759,6 +769,164 @@ static void launch_ws(const dvie_conv_desc& p, hipStream_t s) {
     launch_ws_rows<KS, 4>(p, s);
 }
 
+// ---------------------------------------------------------------------------------------
+// Dense-K variant for 3x3 stride-1 convs with few input channels (c = 8, 16 or 24: the data
+// gradients of the 3- / 20-channel output heads into their 448-channel hidden layers, the
+// 20-channel seg encoder, the image stems).  The chunked kernels give every tap a 64-channel
+// K slice, so c = 8 spends 7/8 of its MFMAs on zeros.  Here K is the flattened (tap,
+// channel) axis of the packed weights, 9c long: a 16-deep MFMA slice covers two 8-channel
+// groups -- lane half h takes group 2s + h, i.e. its own tap -- so c = 8 needs 5 slices per
+// output block instead of 36 (c = 24: 14 instead of 36).
+// * Halo image: CP8 = c/8 slots of 16 B per pixel (pitch 16 B for c = 8, 48 B otherwise: a
+//   16-lane ds_read_b128 group then touches 16 distinct bank quads), LDS-DMA filled,
+//   double-buffered; ~6-19 KB per tile, so several workgroups share a CU.
+// * A workgroup owns one 64-channel output block (weights in VGPRs for all slices, loaded
+//   once) and walks output tiles of 4 rows x 64 pixels; 8 waves = 2 channel halves x 4 rows.
+//   Workgroups of one tile (one per output block) are consecutive logical ids on one XCD,
+//   so the halo is read from HBM once and from L2 by the others.
+template <int CP8>
+struct NkCfg {
+  static constexpr int WP = 4, NW = 8;
+  static constexpr int HR = WP + 2, HWD = 66;
+  static constexpr int PS = CP8 == 1 ? 1 : 3;  // 16-B slots per pixel (pitch)
+  static constexpr int SLOTS = HR * HWD * PS;
+  static constexpr int NPC = ((SLOTS + 63) / 64 + NW - 1) / NW;  // DMA pieces per wave
+  static constexpr int HSZ = NPC * NW * 1024;
+  static constexpr int NG = 9 * CP8;         // 8-channel groups along K
+  static constexpr int NS = (NG + 1) / 2;    // 16-deep MFMA slices
+};
+
+template <int CP8, bool OUTF32>
+__global__ __launch_bounds__(512, 2) void conv_nk_kernel(const dvie_conv_desc p, int n_cb, int n_tiles, int tiles_x,
+                                                        int tiles_y) {
+  typedef NkCfg<CP8> C;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * C::HSZ];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave / C::WP, wp = wave % C::WP;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // logical id: (tile-major, output block fastest), XCD-contiguous ranges
+  const int lid = xcd_remap3(blockIdx.x, gridDim.x);
+  const int cb = lid % n_cb;
+  const int per_cb = gridDim.x / n_cb;  // workgroups per output block (grid = n_cb * per_cb)
+  const int tile0 = lid / n_cb;
+  if (tile0 >= n_tiles) return;
+
+  // weights -> VGPRs: lane (r32, h) holds w[co][16 s + 8 h .. +7] of the flattened K = 9c
+  i32x4 wa[C::NS];
+  {
+    const int co = cb * 64 + 32 * wc + r32;
+#pragma unroll
+    for (int sl = 0; sl < C::NS; ++sl) {
+      const int k = 16 * sl + 8 * hh;
+      i32x4 v = {0, 0, 0, 0};
+      if (co < p.cout && k < 9 * p.c) v = *(const i32x4*)((const bf16_t*)p.w + (long long)co * p.kpad + k);
+      wa[sl] = v;
+    }
+  }
+  // B fragment offsets: group g = 2 s + h -> tap t = g / CP8 (row t/3, column t%3), 16-B
+  // slot g % CP8 of the shifted pixel
+  int boff[C::NS];
+#pragma unroll
+  for (int sl = 0; sl < C::NS; ++sl) {
+    const int g = 2 * sl + hh;
+    const int t = g < C::NG ? g / CP8 : 0, j = g < C::NG ? g % CP8 : 0;
+    boff[sl] = (((t / 3) * C::HWD + (t % 3)) * C::PS + j) * 16;
+  }
+  // DMA geometry: slot -> (halo row, halo column, 16-B channel group)
+  int hgeo[C::NPC];
+#pragma unroll
+  for (int q = 0; q < C::NPC; ++q) {
+    const int slot = (wave + C::NW * q) * 64 + lane;
+    const int px = slot / C::PS, cs = slot - C::PS * (slot / C::PS);
+    const int hy = px / C::HWD, hx = px - (px / C::HWD) * C::HWD;
+    hgeo[q] = (cs < CP8 && cs * 8 < p.c && px < C::HR * C::HWD) ? (hy << 16) | (hx << 4) | cs : -1;
+  }
+  const unsigned xrow = (unsigned)p.x_ld * 2u;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)xbytes, 0x00020000);
+  struct TP {
+    int n, y0, x0;
+  };
+  auto decode = [&](int t) {
+    TP q;
+    q.x0 = (t % tiles_x) * 64;
+    const int r = t / tiles_x;
+    q.y0 = (r % tiles_y) * C::WP;
+    q.n = r / tiles_y;
+    return q;
+  };
+  auto halo_issue = [&](const TP& T, int hb) {
+    char* dst = smem + hb * C::HSZ + wave * 1024;
+    const int ybase = T.y0 + p.dy0, xbase = T.x0 + p.dx0;
+#pragma unroll
+    for (int q = 0; q < C::NPC; ++q) {
+      const int gq = hgeo[q];
+      const int iy = ybase + (gq >> 16), ix = xbase + ((gq >> 4) & 0xFFF);
+      const bool ok = gq >= 0 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw;
+      const unsigned o = ok ? (unsigned)((T.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)(gq & 15) * 16u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(dst + q * C::NW * 1024), 16, o, 0, 0, 0);
+    }
+  };
+
+  const int b_base = ((wp * C::HWD + r32) * C::PS) * 16;
+  TP cur = decode(tile0);
+  halo_issue(cur, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  int hb = 0;
+  for (int tile = tile0; tile < n_tiles; tile += per_cb, hb ^= 1) {
+    const bool has_next = tile + per_cb < n_tiles;
+    const TP nxt = decode(has_next ? tile + per_cb : tile);
+    if (has_next) halo_issue(nxt, hb ^ 1);
+    f32x16 acc[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+    const char* H = smem + hb * C::HSZ + b_base;
+#pragma unroll
+    for (int sl = 0; sl < C::NS; ++sl) {
+      i32x4 bf[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bf[b] = *(const i32x4*)(H + boff[sl] + 32 * b * C::PS * 16);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa[sl]), __builtin_bit_cast(bf16x8, bf[b]),
+                                                         acc[b], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      ws_epilogue<OUTF32>(p, acc[b], cur.n, cur.y0 + wp, cur.x0 + 32 * b + r32, cb * 64 + 32 * wc + 8 * hh);
+    cur = nxt;
+  }
+}
+
+template <int CP8>
+static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
+  typedef NkCfg<CP8> C;
+  const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + C::WP - 1) / C::WP;
+  const int n_tiles = tiles_x * tiles_y * p.n;
+  const int n_cb = (p.cout + 63) / 64;
+  // resident workgroups: two per CU (launch bounds), a whole number per output block
+  int per_cb = 512 / n_cb;
+  if (per_cb < 1) per_cb = 1;
+  if (per_cb > n_tiles) per_cb = n_tiles;
+  const int grid = per_cb * n_cb;
+  if (p.out_f32)
+    hipLaunchKernelGGL((conv_nk_kernel<CP8, true>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
+  else
+    hipLaunchKernelGGL((conv_nk_kernel<CP8, false>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
+}
+
+// DVIE_CONV_NK=0: narrow-input 3x3 convs on the chunked kernels (A/B runs)
+static const bool nk_env_off = getenv("DVIE_CONV_NK") && *getenv("DVIE_CONV_NK") == '0';
+
 // Returns true when the halo kernel took the launch.
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (p.dtype != DVIE_BF16) return false;
@@ -775,6 +943,14 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (((pix - 1) * (unsigned long long)p.x_ld + (unsigned long long)p.c) * 2ull >= 0xFFFFFF00ull) return false;
   int cfg = env_cfg();
   if (cfg == -1) return false;
+  if (t3 && !nk_env_off && cfg == -3 && p.c % 8 == 0 && p.c <= 24 && p.kpad >= 9 * p.c) {
+    switch (p.c / 8) {
+      case 1: launch_nk<1>(p, s); break;
+      case 2: launch_nk<2>(p, s); break;
+      default: launch_nk<3>(p, s); break;
+    }
+    return true;
+  }
   if (t3 && p.c <= 64 && p.cout <= 64 && (cfg == -3 || cfg == 8) && (long long)p.n * p.oh * p.ow >= 65536) {
     // single input chunk, one 64-channel output tile: weights stay in VGPRs
     switch ((p.c + 15) / 16) {
