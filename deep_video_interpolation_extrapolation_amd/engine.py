@@ -55,9 +55,8 @@ class Buffer:
         self.needs_grad = False
         self.producers = []
         self.consumers = []  # (op, region)
-        self.expected = 0
-        self.pending = []
-        self.read_region = None
+        self.expected = {}  # read region key -> number of gradient contributions
+        self.pending = {}  # read region key -> contributions recorded so far
 
     def __repr__(self):
         return f"Buffer({self.name},{self.H}x{self.W}x{self.C})"
@@ -201,6 +200,75 @@ class LinearAsConv:
     @property
     def bias(self):
         return self.lin.bias
+
+
+class StackedConv:
+    """Several convs of one input run as ONE conv whose output channels are the parts'
+    outputs stacked in order (e.g. HRNet's rgb_layer.0 / seg_layer.0, both 1x1 448 -> 448
+    over the same concat: one 448 -> 896 GEMM reads the concat once, and its data gradient
+    sums both heads' contributions in one K = 896 reduction).  The parts' weights must be
+    consecutive in memory, and so must their biases and their .grad views (FlatParams lays
+    the parameters out in `params()` order); `contiguous()` checks it."""
+
+    def __init__(self, parts):
+        self.parts = list(parts)
+        m0 = self.parts[0]
+        self.stride, self.padding = m0.stride, m0.padding
+        self.dilation, self.groups = getattr(m0, "dilation", (1, 1)), m0.groups
+        for m in self.parts:
+            assert (m.stride, m.padding, m.groups, tuple(m.weight.shape[1:])) == \
+                (m0.stride, m0.padding, m0.groups, tuple(m0.weight.shape[1:]))
+            assert (m.bias is None) == (m0.bias is None)
+
+    def params(self):
+        """flat-buffer order: all weights, then all biases"""
+        return [m.weight for m in self.parts] + [m.bias for m in self.parts if m.bias is not None]
+
+    @staticmethod
+    def _stack(ts):
+        t0 = ts[0]
+        shape = (sum(t.shape[0] for t in ts),) + tuple(t0.shape[1:])
+        return torch.as_strided(t0, shape, t0.stride(), t0.storage_offset())
+
+    @staticmethod
+    def _consecutive(ts):
+        return all(b.data_ptr() == a.data_ptr() + a.numel() * a.element_size() and a.is_contiguous() and b.is_contiguous()
+                   and a.dtype == b.dtype for a, b in zip(ts, ts[1:]))
+
+    def contiguous(self, grads=False):
+        ws = [m.weight for m in self.parts]
+        bs = [m.bias for m in self.parts if m.bias is not None]
+        ok = self._consecutive(ws) and (not bs or self._consecutive(bs))
+        if grads:
+            ok = ok and all(t.grad is not None for t in ws + bs) and self._consecutive([t.grad for t in ws]) and (
+                not bs or self._consecutive([t.grad for t in bs]))
+        return ok
+
+    def _view(self, ts):
+        # not (yet) consecutive, e.g. the shape-only lowering before FlatParams lays the
+        # parameters out: a meta tensor of the stacked shape (packing asserts contiguity)
+        if self._consecutive(ts):
+            return self._stack(ts)
+        return torch.empty((sum(t.shape[0] for t in ts),) + tuple(ts[0].shape[1:]), device="meta")
+
+    @property
+    def weight(self):
+        return self._view([m.weight for m in self.parts])
+
+    @property
+    def bias(self):
+        if self.parts[0].bias is None:
+            return None
+        return self._view([m.bias for m in self.parts])
+
+    def grad_ptr(self, which):
+        """device pointer of the stacked gradient of `which` (the first part's .grad)"""
+        ts = [getattr(m, which) for m in self.parts]
+        for t in ts:
+            if t.grad is None:
+                t.grad = torch.zeros_like(t)
+        assert self._consecutive([t.grad for t in ts]), "StackedConv: part gradients are not consecutive"
+        return ts[0].grad.data_ptr()
 
 
 class FuseOp(_Op):
@@ -516,19 +584,23 @@ class Plan:
                 if b.needs_grad:
                     b.g = torch.zeros((self.nb, b.H, b.W, b.C), dtype=self.dtype, device=self.device)
             for b in g.buffers:
-                b.expected = 0
-                b.pending = []
-                b.read_region = None
+                b.expected = {}
+                b.pending = {}
+                b.n_flushed = 0
                 b.done = False
             for op in g.ops:
                 if isinstance(op, FuseOp) and op.detach:
                     continue
                 for r in op.inputs():
                     if r.buf.needs_grad:
-                        r.buf.expected += 1
-                        if r.buf.read_region is None:
-                            r.buf.read_region = r.key()
-                        assert r.buf.read_region == r.key(), f"{r.buf}: consumers read different regions"
+                        r.buf.expected[r.key()] = r.buf.expected.get(r.key(), 0) + 1
+            # consumers of one buffer read the same channel region or disjoint ones (e.g. the
+            # two head convs reading their halves of the stacked head output); each region's
+            # gradient is flushed on its own
+            for b in g.buffers:
+                keys = sorted(b.expected)
+                for (a0, ac), (b0, _) in zip(keys, keys[1:]):
+                    assert a0 + ac <= b0, f"{b}: consumers read overlapping regions {keys}"
         self.l1_out = torch.zeros(max(1, g.n_l1), dtype=torch.float32, device=self.device)
         self.keep.append(self.l1_out)
         self.bn_splits = 1
@@ -581,6 +653,8 @@ class Plan:
         self._pack_descs = descs  # dgrad packs appended during backward build
 
     def _pack_desc(self, lay, dst, rows, kpad, c, mode, taps, cmap_t):
+        if isinstance(lay.m, StackedConv):
+            assert lay.m.contiguous(), f"{lay.name}: stacked parts are not consecutive in memory"
         d = L.PackDesc()
         d.src, d.dst, d.cmap = lay.m.weight.data_ptr(), dst.data_ptr(), cmap_t.data_ptr()
         d.rows, d.kpad, d.c, d.mode = rows, kpad, c, mode
@@ -871,18 +945,28 @@ class Plan:
         (emitter(beta, res_ptr, res_ld, dact, z_ptr, z_ld) -> ops) or an identity
         (`ident` = (ptr, ld) of a gradient region with the same shape)."""
         b = region.buf
-        assert region.key() == b.read_region
-        b.pending.append((emitter, ident))
-        if len(b.pending) == b.expected:
-            self._flush(b)
+        key = region.key()
+        assert key in b.expected, (b, key)
+        pend = b.pending.setdefault(key, [])
+        pend.append((emitter, ident))
+        if len(pend) == b.expected[key]:
+            self._flush(b, key)
 
-    def _flush(self, b):
-        c0, c = b.read_region
+    def _flush(self, b, key):
+        c0, c = key
         region = Region(b, c0, c)
-        kernels = [e for e, i in b.pending if e is not None]
-        idents = [i for e, i in b.pending if e is None]
+        pending = b.pending.pop(key)
+        kernels = [e for e, i in pending if e is not None]
+        idents = [i for e, i in pending if e is None]
         prod = b.producers
-        fuse_dact = (len(prod) == 1 and prod[0].act != L.ACT_NONE and prod[0].out.key() == b.read_region)
+        # the producer's activation derivative rides on the last contribution of each region
+        # when one activated producer wrote the buffer and the read regions tile its output
+        # exactly (else _ensure_dact applies it in a pass of its own)
+        fuse_dact = False
+        if len(prod) == 1 and prod[0].act != L.ACT_NONE and prod[0].out.buf is b:
+            o0, oc = prod[0].out.c0, prod[0].out.c
+            fuse_dact = (all(o0 <= k0 and k0 + kc <= o0 + oc for k0, kc in b.expected) and
+                         sum(kc for _, kc in b.expected) == oc)
         b.dact_done = fuse_dact
         dact = prod[0].act if fuse_dact else 0
         z = self.ptr(region) if fuse_dact else None
@@ -910,8 +994,8 @@ class Plan:
             ops = em(0 if i == 0 else 1, r[0] if r else None, r[1] if r else 0, dact if last else 0,
                      z if last else None, b.C if last else 0)
             self.bwd.extend(ops)
-        b.done = True
-        b.pending = []
+        b.n_flushed += 1
+        b.done = b.n_flushed == len(b.expected)
 
     def _ensure_dact(self, op):
         """Producer-side activation derivative when it could not be fused upstream."""
@@ -934,7 +1018,7 @@ class Plan:
                 self._uses_left[op.layer] = self._uses_left.get(op.layer, 0) + 1
         for key, (region, ch) in g.outputs.items():
             b = region.buf
-            assert b.needs_grad and b.expected == 0
+            assert b.needs_grad and not b.expected
             assert b.t is not None or all(p.act == L.ACT_NONE for p in b.producers), "external output with activation"
             o = self.ew_desc(L.EW_NCHW, nb, region.H, region.W, region.c, self.ptr(region, grad=True), b.C)
             o.u.ew.ext_c = ch
@@ -1062,7 +1146,8 @@ class Plan:
         # (buffers whose contributions never completed would indicate a graph bug)
         for bf in g.buffers:
             if bf.needs_grad and bf.expected and not getattr(bf, "done", False):
-                raise RuntimeError(f"incomplete gradient for {bf}: {len(bf.pending)}/{bf.expected}")
+                raise RuntimeError(f"incomplete gradient for {bf}: pending {({k: len(v) for k, v in bf.pending.items()})}"
+                                   f" of {bf.expected}")
 
     def _conv_backward(self, op, gout, gld):
         lay, x, out = op.layer, op.x, op.out
@@ -1376,11 +1461,14 @@ class Plan:
                     setattr(d, field, p.grad.data_ptr())
                 d.accumulate = int(accumulate) if first else 1
                 continue
-            p = getattr(lay.m, which)
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
             d = self.bwd_arr[idx].u.wreduce
-            d.dw = p.grad.data_ptr()
+            if isinstance(lay.m, StackedConv):
+                d.dw = lay.m.grad_ptr(which)
+            else:
+                p = getattr(lay.m, which)
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                d.dw = p.grad.data_ptr()
             if first:
                 d.beta = 0 if (which == "weight" and id(lay.m) in fresh) else int(accumulate)
 

@@ -12,6 +12,8 @@ Layout: activations NHWC in the compute dtype (fp32 parity mode or bf16), channe
 padded to multiples of 8; the 14-channel stem input is laid out as
 [segA(4) 0000 segB(4) 0000 rgb(6) 00] and the stem weights are packed to match.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -252,6 +254,9 @@ class HRNet(FlatParams, nn.Module):
         g = self._lower(E.Graph(torch.float32), 16, 16, dry=True)
         order = []
         for lay in reversed(g.layers):
+            if isinstance(lay.m, E.StackedConv):
+                order += lay.m.params()
+                continue
             order.append(lay.m.weight)
             if lay.m.bias is not None:
                 order.append(lay.m.bias)
@@ -274,6 +279,7 @@ class HRNet(FlatParams, nn.Module):
 
     def _lower(self, g, H, W, dry=False, xgrad=False, vgrad=False):
         A = L
+        g.dry = dry
         rup = E.rup
         F = self.n_frames
         segs = []
@@ -431,18 +437,32 @@ class HRNet(FlatParams, nn.Module):
             srcs = [E.R(t)] + srcs[3:]
         g.fuse(srcs, out, act=act)
 
+    # DVIE_FUSE_HEADS=0: the two 1x1 head convs as separate launches (A/B runs)
+    fuse_heads = os.environ.get("DVIE_FUSE_HEADS", "1") != "0"
+
     def _heads(self, g, cat):
+        """rgb_layer / seg_layer (nets/HRNet.py:410-442 of the reference).  Both start with a
+        1x1 448 -> 448 conv + LeakyReLU over the same concat: run as one stacked 448 -> 896
+        conv (E.StackedConv) whose halves feed the two 3x3 output convs."""
         A = L
         H, W = cat.H, cat.W
         last = cat.c
-        hr = g.buffer("rgb_hidden", H, W, last)
-        g.conv(cat, self.rgb_layer[0], E.R(hr), act=A.ACT_LRELU, name="rgb_layer.0")
-        hs = g.buffer("seg_hidden", H, W, last)
-        g.conv(cat, self.seg_layer[0], E.R(hs), act=A.ACT_LRELU, name="seg_layer.0")
+        if getattr(self, "_stacked_heads", None) is None:
+            self._stacked_heads = E.StackedConv([self.rgb_layer[0], self.seg_layer[0]]) if self.fuse_heads else False
+        st = self._stacked_heads
+        if st and (getattr(g, "dry", False) or st.contiguous()):
+            hh = g.buffer("heads_hidden", H, W, 2 * last)
+            g.conv(cat, st, E.R(hh), act=A.ACT_LRELU, name="heads.0")
+            hr, hs = E.R(hh, 0, last), E.R(hh, last, last)
+        else:
+            hr = E.R(g.buffer("rgb_hidden", H, W, last))
+            g.conv(cat, self.rgb_layer[0], hr, act=A.ACT_LRELU, name="rgb_layer.0")
+            hs = E.R(g.buffer("seg_hidden", H, W, last))
+            g.conv(cat, self.seg_layer[0], hs, act=A.ACT_LRELU, name="seg_layer.0")
         rgb = g.buffer("rgb", H, W, E.rup(self.rgb_out_dim, 8), dtype=torch.float32, external=True)
-        g.conv(E.R(hr), self.rgb_layer[2], E.R(rgb), name="rgb_layer.2")
+        g.conv(hr, self.rgb_layer[2], E.R(rgb), name="rgb_layer.2")
         seg = g.buffer("segout", H, W, E.rup(self.seg_out_dim, 8), dtype=torch.float32, external=True)
-        g.conv(E.R(hs), self.seg_layer[2], E.R(seg), name="seg_layer.2")
+        g.conv(hs, self.seg_layer[2], E.R(seg), name="seg_layer.2")
         g.output("rgb", E.R(rgb), self.rgb_out_dim)
         g.output("segout", E.R(seg), self.seg_out_dim)
 
@@ -502,7 +522,10 @@ class HRNet(FlatParams, nn.Module):
         total = self._flat.numel()
         cuts, ranges, last, hi, done = [], [], 0, 0, 0
         for idx, lay in plan.completions:
-            ps = [lay.m.weight] + ([lay.m.bias] if lay.m.bias is not None else [])
+            if isinstance(lay.m, E.StackedConv):
+                ps = lay.m.params()
+            else:
+                ps = [lay.m.weight] + ([lay.m.bias] if lay.m.bias is not None else [])
             hi = max([hi] + [end[id(p)] for p in ps])
             done += sum(p.numel() for p in ps)
             assert done == hi, "parameter gradients must complete in flat-buffer order"

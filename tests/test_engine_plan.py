@@ -39,16 +39,27 @@ def test_params_are_views_of_one_flat_buffer():
         assert base <= p.data_ptr() < end
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_hrnet_plan_structure(dtype):
+def test_hrnet_plan_structure(dtype, fused, monkeypatch):
+    """77 reference convs; with the two 1x1 head convs stacked into one 448 -> 896 conv
+    (E.StackedConv, the default) the plan has 76, and the stacked output's two halves --
+    read by rgb_layer.2 and seg_layer.2 -- each receive their gradient."""
+    from deep_video_interpolation_extrapolation_amd.nets.HRNet import HRNet
+    monkeypatch.setattr(HRNet, "fuse_heads", fused)
     hr = make().coarse_model
     g = hr._lower(E.Graph(dtype), 32, 64)
     plan = g.compile(2, torch.device("cpu"), backward=True)
     kinds = plan.describe()["kinds"]
     n_conv_fwd = sum(1 for op in g.ops if isinstance(op, E.ConvOp))
-    assert n_conv_fwd == 77
+    n_ref = 76 if fused else 77
+    assert n_conv_fwd == n_ref
+    heads = [b for b in g.buffers if b.name == "heads_hidden"]
+    assert len(heads) == int(fused)
+    if fused:
+        assert sorted(heads[0].expected) == [(0, 448), (448, 448)] and heads[0].dact_done
     # every trainable conv gets one wgrad; stride-2 dgrads split into 4 phases
-    assert kinds[L.OP_WGRAD] == 77
+    assert kinds[L.OP_WGRAD] == n_ref
     n_s2 = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2)
     n_dgrad = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.x.buf.needs_grad)
     assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2
