@@ -450,7 +450,12 @@ class HRNet(FlatParams, nn.Module):
         if getattr(self, "_stacked_heads", None) is None:
             self._stacked_heads = E.StackedConv([self.rgb_layer[0], self.seg_layer[0]]) if self.fuse_heads else False
         st = self._stacked_heads
-        if st and (getattr(g, "dry", False) or st.contiguous()):
+        # the 3x3 output convs address one image of the stacked buffer through a 32-bit
+        # buffer range: keep the two hidden maps separate where 2x448 channels exceed it
+        # (fp32 at 1024x2048)
+        es = 2 if g.dtype == torch.bfloat16 else 4
+        fits = H * W * 2 * last * es < 0xFFFFFF00
+        if st and fits and (getattr(g, "dry", False) or st.contiguous()):
             hh = g.buffer("heads_hidden", H, W, 2 * last)
             g.conv(cat, st, E.R(hh), act=A.ACT_LRELU, name="heads.0")
             hr, hs = E.R(hh, 0, last), E.R(hh, last, last)

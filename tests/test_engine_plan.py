@@ -69,6 +69,16 @@ def test_hrnet_plan_structure(dtype, fused, monkeypatch):
             assert b.done
 
 
+@pytest.mark.parametrize("dtype,stacked", [(torch.float32, False), (torch.bfloat16, True)])
+def test_stacked_heads_fit_the_buffer_range(dtype, stacked):
+    """At 1024x2048 the stacked 896-channel hidden map is 7.5 GB per image in fp32, past
+    the 32-bit buffer range the 3x3 output convs address one image through: the heads
+    stay separate there (bf16: 3.8 GB, stacked)."""
+    hr = make().coarse_model
+    g = hr._lower(E.Graph(dtype), 1024, 2048)
+    assert any(b.name == "heads_hidden" for b in g.buffers) == stacked
+
+
 def test_highres_large_builds():
     hr = make(highres_large=True).coarse_model
     g = hr._lower(E.Graph(torch.float32), 32, 64)
