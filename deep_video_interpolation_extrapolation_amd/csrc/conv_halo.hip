@@ -106,27 +106,18 @@ struct HaloCfg {
 #define DVIE_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
-    case 0: DVIE_VMCNT(0); break;
-    case 1: DVIE_VMCNT(1); break;
-    case 2: DVIE_VMCNT(2); break;
-    case 3: DVIE_VMCNT(3); break;
-    case 4: DVIE_VMCNT(4); break;
-    case 5: DVIE_VMCNT(5); break;
-    case 6: DVIE_VMCNT(6); break;
-    case 7: DVIE_VMCNT(7); break;
-    case 8: DVIE_VMCNT(8); break;
-    case 9: DVIE_VMCNT(9); break;
-    case 10: DVIE_VMCNT(10); break;
-    case 11: DVIE_VMCNT(11); break;
-    case 12: DVIE_VMCNT(12); break;
-    case 13: DVIE_VMCNT(13); break;
-    case 14: DVIE_VMCNT(14); break;
-    case 15: DVIE_VMCNT(15); break;
-    case 16: DVIE_VMCNT(16); break;
-    case 17: DVIE_VMCNT(17); break;
-    case 18: DVIE_VMCNT(18); break;
-    case 19: DVIE_VMCNT(19); break;
-    case 20: DVIE_VMCNT(20); break;
+#define DVIE_VMCASE(N) \
+  case N:              \
+    DVIE_VMCNT(N);     \
+    break;
+    DVIE_VMCASE(0) DVIE_VMCASE(1) DVIE_VMCASE(2) DVIE_VMCASE(3) DVIE_VMCASE(4) DVIE_VMCASE(5) DVIE_VMCASE(6)
+    DVIE_VMCASE(7) DVIE_VMCASE(8) DVIE_VMCASE(9) DVIE_VMCASE(10) DVIE_VMCASE(11) DVIE_VMCASE(12) DVIE_VMCASE(13)
+    DVIE_VMCASE(14) DVIE_VMCASE(15) DVIE_VMCASE(16) DVIE_VMCASE(17) DVIE_VMCASE(18) DVIE_VMCASE(19) DVIE_VMCASE(20)
+    DVIE_VMCASE(21) DVIE_VMCASE(22) DVIE_VMCASE(23) DVIE_VMCASE(24) DVIE_VMCASE(25) DVIE_VMCASE(26) DVIE_VMCASE(27)
+    DVIE_VMCASE(28) DVIE_VMCASE(29) DVIE_VMCASE(30) DVIE_VMCASE(31) DVIE_VMCASE(32) DVIE_VMCASE(33) DVIE_VMCASE(34)
+    DVIE_VMCASE(35) DVIE_VMCASE(36) DVIE_VMCASE(37) DVIE_VMCASE(38) DVIE_VMCASE(39) DVIE_VMCASE(40) DVIE_VMCASE(41)
+    DVIE_VMCASE(42) DVIE_VMCASE(43) DVIE_VMCASE(44) DVIE_VMCASE(45) DVIE_VMCASE(46) DVIE_VMCASE(47) DVIE_VMCASE(48)
+#undef DVIE_VMCASE
     default: DVIE_VMCNT(0); break;
   }
 }
@@ -137,7 +128,8 @@ struct JobInfo {
 
 template <int TM, int WC, int WP, int TH, int TW, bool OUTF32>
 __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_desc p, int n_ct, int n_tiles,
-                                                                 int tiles_x, int tiles_y, int persistent) {
+                                                                 int tiles_x, int tiles_y, int persistent,
+                                                                 int epi_pre) {
   typedef HaloCfg<TM, WC, WP, TH, TW> C;
   constexpr int NW = C::NW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
@@ -259,6 +251,44 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   }
   const int b_base = (wp * C::HWD + r32) * C::PITCH + hh * 16;
 
+  // ---- epilogue operands (bf16 output): residual, accumulate target and activation input
+  // of the tile are loaded into registers during its last chunk, PRE_T steps before the
+  // epilogue, so their HBM latency overlaps the remaining MFMAs instead of following them.
+  // Buffer loads from a per-tile base: every wave issues the same count (lanes outside the
+  // output get an out-of-range offset and load zeros), so the step's vmcnt stays exact.
+  constexpr int PRE_T = C::NT >= 2 ? C::NT - 2 : 0;
+  const bool PRE = !OUTF32 && epi_pre;
+  const int npre = PRE ? TM * 4 * ((p.res ? 1 : 0) + (p.beta ? 1 : 0) + (p.dact ? 1 : 0)) : 0;
+  i32x4 pre_r[TM][2][2], pre_b[TM][2][2], pre_z[TM][2][2];
+  auto epi_prefetch = [&](const JobInfo& Jt) {
+    const long long pix0 = ((long long)Jt.n * p.yh + (long long)Jt.y0 * p.osy + p.ory) * p.yw + (long long)Jt.x0 * p.osx + p.orx;
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16_t*)p.res + (p.res ? pix0 * p.res_ld : 0)), 0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16_t*)p.y + pix0 * p.y_ld), 0, 0x7FFFFFF0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rz =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16_t*)p.z + (p.dact ? pix0 * p.z_ld : 0)), 0, 0x7FFFFFF0, 0x00020000);
+    const int oy = Jt.y0 + wp;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          const int ox = Jt.x0 + 32 * b + r32;
+          const int co = Jt.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh;
+          const bool ok = oy < p.oh && ox < p.ow && co < p.cout;
+          const long long dp = (long long)wp * p.osy * p.yw + (long long)(32 * b + r32) * p.osx;
+          const unsigned OFF = 0xFFFFFFF0u;
+          if (p.res)
+            pre_r[i][b][P] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? (unsigned)((dp * p.res_ld + co) * 2) : OFF, 0, 0);
+          if (p.beta)
+            pre_b[i][b][P] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? (unsigned)((dp * p.y_ld + co) * 2) : OFF, 0, 0);
+          if (p.dact)
+            pre_z[i][b][P] = __builtin_amdgcn_raw_buffer_load_b128(rz, ok ? (unsigned)((dp * p.z_ld + co) * 2) : OFF, 0, 0);
+        }
+  };
+
   // ---- prologue: job 0 halo (+ job 1 for 1x1), weights of steps 0 and 1 ----
   {
     const JobInfo J0 = tile_job(tile0);
@@ -331,6 +361,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
           else
             halo_issue(J2, (j + 2) % C::NH, 0, C::NHQ);
         }
+        if (PRE && s == 1 && t == PRE_T && J.k + 1 == nchunks) epi_prefetch(J);
         __builtin_amdgcn_sched_barrier(0);
         const int fb = s & 1;
 #pragma unroll
@@ -342,8 +373,9 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
                                                                 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      // everything issued before this step has landed (this step's loads may stay in flight)
-      wait_vmcnt(issued);
+      // everything issued before this step has landed (this step's loads may stay in flight;
+      // the epilogue prefetch, issued last, too)
+      wait_vmcnt(issued + (PRE && t == PRE_T && J.k + 1 == nchunks ? npre : 0));
       // plain s_barrier: __syncthreads() would add a release fence, i.e. vmcnt(0)
       __builtin_amdgcn_s_barrier();
     }
@@ -418,7 +450,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
           } else {
             bf16_t* dst = (bf16_t*)p.y + pix * p.y_ld + co;
             if (p.res) {
-              const i32x4 tr = *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
+              const i32x4 tr = PRE ? pre_r[i][b][P] : *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
@@ -426,7 +458,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
               }
             }
             if (p.beta) {
-              const i32x4 tr = *(const i32x4*)dst;
+              const i32x4 tr = PRE ? pre_b[i][b][P] : *(const i32x4*)dst;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
@@ -436,7 +468,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
             act_apply(w, 8, p.act, p.alpha);
             if (p.dact) {
               float z[8];
-              const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
+              const i32x4 tz = PRE ? pre_z[i][b][P] : *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 z[2 * e] = __uint_as_float(((uint32_t)tz[e]) << 16);
@@ -453,6 +485,9 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
       }
   }
 }
+
+// DVIE_EPI_PREFETCH=0: epilogue operands loaded in the epilogue (A/B runs)
+static const bool epi_prefetch_on = !(getenv("DVIE_EPI_PREFETCH") && *getenv("DVIE_EPI_PREFETCH") == '0');
 
 template <int TM, int WC, int WP, int TH, int TW>
 static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
@@ -471,10 +506,10 @@ static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
     const int grid = persistent ? cap : n_tiles;
     if (p.out_f32)
       hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
-                         n_tiles, tiles_x, tiles_y, persistent);
+                         n_tiles, tiles_x, tiles_y, persistent, 0);
     else
       hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, false>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
-                         n_tiles, tiles_x, tiles_y, persistent);
+                         n_tiles, tiles_x, tiles_y, persistent, epi_prefetch_on ? 1 : 0);
     return true;
   }
 }

@@ -1,0 +1,89 @@
+"""Conv epilogue operands through the C ABI (dvie_conv2d_fwd), every combination of
+residual / accumulate (beta) / activation / activation derivative, on the kernels the
+library picks by shape: weight-stationary 3x3 (c, cout <= 64, >= 65536 output pixels),
+the chunked halo kernel (128- and 64-channel output tiles), the dense-K kernel (c <= 24)
+and the 1x1 GEMM.  Ragged output sizes put lanes past the image edge in every tile row.
+
+Reference: bf16-rounded operands, conv in fp32 (torch CPU), the same epilogue order
+(acc + bias + res + y_old -> act -> dact(z)); tolerance 1e-2 relative to max |y| (bf16
+output rounding, fp32 accumulation)."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deep_video_interpolation_extrapolation_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # n, H, W, c, cout, k
+    (2, 131, 250, 64, 64, 3),   # conv_ws
+    (1, 67, 200, 32, 32, 3),    # conv_ws is skipped below 65536 px: halo cfg 2
+    (2, 35, 90, 128, 128, 3),   # halo 128-channel tiles
+    (2, 35, 90, 256, 64, 3),    # halo 64-channel tiles, 4 chunks
+    (2, 40, 70, 16, 64, 3),     # dense-K
+    (2, 37, 77, 128, 256, 1),   # 1x1
+]
+MODES = ["none", "res", "beta", "z", "res+z", "beta+z", "res+beta+z"]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _lrelu(v):
+    return torch.where(v > 0, v, 0.2 * v)
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_epilogue_operands(dev, shape, mode):
+    n, H, W, c, cout, k = shape
+    g = torch.Generator().manual_seed(7)
+    x = _bf(torch.randn(n, H, W, c, generator=g))
+    wt = _bf(torch.randn(cout, c, k, k, generator=g) / (c * k * k) ** 0.5)
+    bias = torch.randn(cout, generator=g) * 0.1
+    res = _bf(torch.randn(n, H, W, cout, generator=g)) if "res" in mode else None
+    yold = _bf(torch.randn(n, H, W, cout, generator=g)) if "beta" in mode else None
+    z = _bf(torch.randn(n, H, W, cout, generator=g)) if "z" in mode else None
+    act = L.ACT_LRELU if mode in ("none", "res", "beta") else L.ACT_NONE
+
+    ref = F.conv2d(x.permute(0, 3, 1, 2), wt, bias, padding=k // 2).permute(0, 2, 3, 1)
+    if res is not None:
+        ref = ref + res
+    if yold is not None:
+        ref = ref + yold
+    if act == L.ACT_LRELU:
+        ref = _lrelu(ref)
+    if z is not None:
+        ref = ref * torch.where(z > 0, 1.0, 0.2)
+
+    K = k * k * c
+    kpad = (K + 63) // 64 * 64
+    wp = torch.zeros(cout, kpad)
+    wp[:, :K] = wt.permute(0, 2, 3, 1).reshape(cout, K)  # [co][tap * c + ci]
+    xd = x.to(torch.bfloat16).to(dev)
+    wd = wp.to(torch.bfloat16).to(dev)
+    bd = bias.to(dev)
+    yd = (yold if yold is not None else torch.zeros(n, H, W, cout)).to(torch.bfloat16).to(dev)
+    rd = res.to(torch.bfloat16).to(dev) if res is not None else None
+    zd = z.to(torch.bfloat16).to(dev) if z is not None else None
+
+    d = L.ConvDesc()
+    d.x, d.w, d.y, d.bias = xd.data_ptr(), wd.data_ptr(), yd.data_ptr(), bd.data_ptr()
+    d.res = rd.data_ptr() if rd is not None else None
+    d.z = zd.data_ptr() if zd is not None else None
+    d.x_ld, d.y_ld, d.res_ld, d.z_ld = c, cout, cout, cout
+    d.n, d.ih, d.iw, d.c, d.kpad, d.cout = n, H, W, c, kpad, cout
+    d.oh, d.ow, d.sy, d.sx = H, W, 1, 1
+    d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = k, k, -(k // 2), -(k // 2), 1, 1
+    d.yh, d.yw, d.osy, d.osx, d.ory, d.orx = H, W, 1, 1, 0, 0
+    d.act, d.dact, d.beta = act, L.ACT_LRELU if z is not None else L.ACT_NONE, int(yold is not None)
+    d.dtype, d.out_f32, d.alpha = L.BF16, 0, 0.2
+    L.check(L.load().dvie_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+            "conv")
+    torch.cuda.synchronize()
+    out = yd.float().cpu()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2, (shape, mode, err)
