@@ -805,6 +805,301 @@ static void launch_ws(const dvie_conv_desc& p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Strip variant of the weight-stationary 3x3 conv (c <= 64, cout <= 64).  conv_ws_kernel
+// stages a (WP+2)-row halo per WP output rows, so every input row is fetched 1.5-2x, and it
+// prefetches one tile ahead, which does not cover HBM latency at two waves per SIMD.  Here a
+// workgroup owns a 64-pixel column strip of a segment of SEG output rows and walks down it:
+// the input rows live in an LDS ring, each row is fetched ONCE per segment (row overhead
+// (SEG+2)/SEG, column overhead 66/64), and the rows of iteration i+D are issued at the start
+// of iteration i, D iterations of MFMA work ahead of their use.
+// * Ring row: 66 pixels x 144 B (8 data slots + 1 pad slot, conflict-free tap-shifted
+//   ds_read_b128 as in the halo kernels), filled by 10 LDS-DMA pieces of 1 KiB.
+// * Iteration i computes output rows i*WR .. i*WR+WR-1 of the segment (one per row-wave,
+//   two channel halves of 32), from ring rows i*WR .. i*WR+WR+1.  Group i loads rows
+//   i*WR+2 .. i*WR+WR+1 (the two leading rows are a prologue group), so with
+//   RR = WR+2+D*WR ring rows, group i+D overwrites only rows of iterations < i.
+// * One barrier per iteration: after it, every wave's DMA of group i has landed and every
+//   wave is done with iteration i-1.  Groups past the segment end are issued against an
+//   empty buffer range (no traffic), so every wave's vmcnt bookkeeping is compile-time.
+template <int WR, int D>
+struct StripCfg {
+  static constexpr int NW = 2 * WR;
+  static constexpr int HWD = 66, PITCH = 144;
+  static constexpr int RP = (HWD * 9 + 63) / 64;        // DMA pieces per ring row (10)
+  static constexpr int RB = RP * 1024;                   // bytes per ring row
+  static constexpr int RR = WR + 2 + D * WR;             // ring rows
+  static constexpr int NPL = RP * WR / NW;               // pieces per wave per group (5)
+  static constexpr int NP0 = (2 * RP + NW - 1) / NW;     // pieces per wave, prologue rows
+  static constexpr int JUNK = NP0 * NW - 2 * RP;         // prologue pieces with no row
+  static constexpr int SMEM = RR * RB + JUNK * 1024;
+  static_assert(RP * WR % NW == 0, "uniform pieces per wave");
+};
+
+// bf16 epilogue of one 32x32 accumulator block from operands prefetched into registers
+// (EPI: 1 residual, 2 accumulate target, 4 activation input; i32x4 [pair P] each)
+template <int EPI>
+__device__ __forceinline__ void strip_epilogue(const dvie_conv_desc& p, const f32x16& acc, int n, int oy, int ox, int co8,
+                                               const i32x4* er, const i32x4* eb, const i32x4* ez) {
+  float v[2][8];
+#pragma unroll
+  for (int P = 0; P < 2; ++P)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[8 * P + e]), __float_as_uint(acc[8 * P + 4 + e]),
+                                                       false, false);
+      v[P][e] = __uint_as_float(sw[0]);
+      v[P][4 + e] = __uint_as_float(sw[1]);
+    }
+  if (oy >= p.oh || ox >= p.ow) return;
+  const long long pix = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+#pragma unroll
+  for (int P = 0; P < 2; ++P) {
+    const int co = co8 + 16 * P;
+    if (co >= p.cout) continue;
+    float* w = v[P];
+    if (p.bias) {
+      const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w[e] += b0[e];
+        w[4 + e] += b1[e];
+      }
+    }
+    auto add_bf = [&](const i32x4 t) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w[2 * e] += __uint_as_float(((uint32_t)t[e]) << 16);
+        w[2 * e + 1] += __uint_as_float(((uint32_t)t[e]) & 0xffff0000u);
+      }
+    };
+    if constexpr ((EPI & 1) != 0) add_bf(er[P]);
+    if constexpr ((EPI & 2) != 0) add_bf(eb[P]);
+    act_apply(w, 8, p.act, p.alpha);
+    if constexpr ((EPI & 4) != 0) {
+      float z[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        z[2 * e] = __uint_as_float(((uint32_t)ez[P][e]) << 16);
+        z[2 * e + 1] = __uint_as_float(((uint32_t)ez[P][e]) & 0xffff0000u);
+      }
+      dact_apply(w, z, 8, p.dact, p.alpha);
+    }
+    i32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
+    *(i32x4*)((bf16_t*)p.y + pix * p.y_ld + co) = o;
+  }
+}
+
+// EPI < 0: fp32 output, operands read in the epilogue (parity mode, not tuned)
+template <int KS, int EPI, int WR, int D>
+__global__ __launch_bounds__(2 * WR * 64, 4 / WR) void conv_strip_kernel(const dvie_conv_desc p, int tiles_x, int nseg,
+                                                                          int seg, int n_wg) {
+  typedef StripCfg<WR, D> C;
+  constexpr int NW = C::NW;
+  constexpr bool OUTF32 = EPI < 0;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave / WR, wr = wave % WR;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // logical id: segments of one strip consecutive (they share boundary rows in L2)
+  const int lid = xcd_remap3(blockIdx.x, n_wg);
+  const int sg = lid % nseg;
+  const int strip = (lid / nseg) % tiles_x;
+  const int n = lid / nseg / tiles_x;
+  const int ys = sg * seg, x0 = strip * 64;
+  if (ys >= p.oh) return;
+  const int niter = (min(seg, p.oh - ys) + WR - 1) / WR;
+
+  // ---- weights -> VGPRs (as conv_ws_kernel)
+  i32x4 wa[9][KS];
+  {
+    const int co = 32 * wc + r32;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int sl = 0; sl < KS; ++sl) {
+        const int k = 16 * sl + 8 * hh;
+        i32x4 v = {0, 0, 0, 0};
+        if (co < p.cout && k < p.c) v = *(const i32x4*)((const bf16_t*)p.w + (long long)co * p.kpad + t * p.c + k);
+        wa[t][sl] = v;
+      }
+  }
+
+  // ---- DMA: piece pc of a group -> (row j in the group, 1-KiB piece pr of the ring row)
+  const unsigned xrow = (unsigned)p.x_ld * 2u;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const int xb = x0 + p.dx0, yb = ys + p.dy0;  // input column of ring pixel 0, input row of ring row 0
+  auto lane_off = [&](int pr, int iy) -> unsigned {
+    const int slot = pr * 64 + lane;
+    const int px = slot / 9, cs = slot - 9 * (slot / 9);
+    const int ix = xb + px;
+    const bool ok = px < C::HWD && cs < 8 && cs * 8 < p.c && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw;
+    return ok ? (unsigned)((n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)cs * 16u : OOB;
+  };
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rnone = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, 0, 0x00020000);
+  // group g: ring rows R = g*WR+2+j, j < WR (rows past the segment: empty range, no traffic)
+  auto group_issue = [&](int g) {
+    const __amdgpu_buffer_rsrc_t r = g < niter ? rx : rnone;
+#pragma unroll
+    for (int q = 0; q < C::NPL; ++q) {
+      const int pc = wave + NW * q;
+      const int j = pc / C::RP, pr = pc - C::RP * (pc / C::RP);
+      const int R = g * WR + 2 + j;
+      char* dst = smem + (R % C::RR) * C::RB + pr * 1024;
+      // (offset as a separate statement: see halo_issue)
+      const unsigned o = lane_off(pr, yb + R);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, o, 0, 0, 0);
+    }
+  };
+  {  // prologue: ring rows 0 and 1 (pieces without a row land in the junk area), groups 0..D-1
+#pragma unroll
+    for (int q = 0; q < C::NP0; ++q) {
+      const int pc = wave + NW * q;
+      const int j = pc / C::RP, pr = pc - C::RP * (pc / C::RP);
+      char* dst = pc < 2 * C::RP ? smem + j * C::RB + pr * 1024 : smem + C::RR * C::RB + (pc - 2 * C::RP) * 1024;
+      const unsigned o = pc < 2 * C::RP ? lane_off(pr, yb + j) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)dst, 16, o, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < D; ++g) group_issue(g);
+  }
+
+  // epilogue operands of iteration i, issued before group i+D so that waiting for them never
+  // waits for the look-ahead rows
+  constexpr int NE = OUTF32 ? 0 : 4 * (((EPI & 1) ? 1 : 0) + ((EPI & 2) ? 1 : 0) + ((EPI & 4) ? 1 : 0));
+  i32x4 er[2][2], eb[2][2], ez[2][2];
+  auto epi_issue = [&](int i) {
+    const int oy = ys + i * WR + wr;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        const int ox = x0 + 32 * b + r32, co = 32 * wc + 8 * hh + 16 * P;
+        const bool ok = oy < p.oh && ox < p.ow && co < p.cout;
+        const long long pix = ((long long)n * p.yh + (long long)oy * p.osy + p.ory) * p.yw + (long long)ox * p.osx + p.orx;
+        if constexpr ((EPI & 1) != 0) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p.res, 0, 0x7FFFFFF0, 0x00020000);
+          er[b][P] = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (unsigned)((pix * p.res_ld + co) * 2) : OOB, 0, 0);
+        }
+        if constexpr ((EPI & 2) != 0) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p.y, 0, 0x7FFFFFF0, 0x00020000);
+          eb[b][P] = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (unsigned)((pix * p.y_ld + co) * 2) : OOB, 0, 0);
+        }
+        if constexpr ((EPI & 4) != 0) {
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p.z, 0, 0x7FFFFFF0, 0x00020000);
+          ez[b][P] = __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (unsigned)((pix * p.z_ld + co) * 2) : OOB, 0, 0);
+        }
+      }
+  };
+
+  constexpr int NST = OUTF32 ? 8 : 4;  // epilogue stores per wave per iteration (at most)
+  const int b_lane = r32 * C::PITCH + hh * 16;
+  for (int i = 0; i < niter; ++i) {
+    // groups <= i landed; in flight may stay: groups i+1 .. i+D-1, the stores of the last
+    // min(i, D) iterations, the epilogue operands of the last min(i, D-1) iterations
+    wait_vmcnt((D - 1) * C::NPL + min(i, D) * NST + min(i, D - 1) * NE);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (NE > 0) epi_issue(i);
+    group_issue(i + D);
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+#pragma unroll
+    for (int ti = 0; ti < 3; ++ti) {
+      const char* H = smem + ((i * WR + wr + ti) % C::RR) * C::RB + b_lane;
+#pragma unroll
+      for (int tj = 0; tj < 3; ++tj)
+#pragma unroll
+        for (int sl = 0; sl < KS; ++sl) {
+          i32x4 bf[2];
+#pragma unroll
+          for (int b = 0; b < 2; ++b) bf[b] = *(const i32x4*)(H + (32 * b + tj) * C::PITCH + sl * 32);
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa[3 * ti + tj][sl]),
+                                                             __builtin_bit_cast(bf16x8, bf[b]), acc[b], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if constexpr (OUTF32)
+        ws_epilogue<true>(p, acc[b], n, ys + i * WR + wr, x0 + 32 * b + r32, 32 * wc + 8 * hh);
+      else
+        strip_epilogue<(EPI < 0 ? 0 : EPI)>(p, acc[b], n, ys + i * WR + wr, x0 + 32 * b + r32, 32 * wc + 8 * hh, er[b], eb[b],
+                                          ez[b]);
+    }
+  }
+  // drain: no DMA may still target this workgroup's LDS when it exits
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+template <int KS, int WR, int D, int EPI>
+static void launch_strip_k(const dvie_conv_desc& p, hipStream_t s) {
+  const int tiles_x = (p.ow + 63) / 64;
+  const int cap = 256 * (4 / WR);  // resident workgroups
+  const int cols = p.n * tiles_x;
+  int nseg = cap / cols;
+  if (nseg < 1) nseg = 1;
+  if (nseg > (p.oh + WR - 1) / WR) nseg = (p.oh + WR - 1) / WR;
+  int seg = (p.oh + nseg - 1) / nseg;
+  seg = (seg + WR - 1) / WR * WR;
+  nseg = (p.oh + seg - 1) / seg;
+  const int n_wg = cols * nseg;
+  hipLaunchKernelGGL((conv_strip_kernel<KS, EPI, WR, D>), dim3(n_wg), dim3(2 * WR * 64), 0, s, p, tiles_x, nseg, seg,
+                     n_wg);
+}
+
+// epilogue-operand set of a launch -> kernel instance (fp32 output: EPI -1)
+// (all three operands: not taken -- their registers do not fit next to the weights)
+template <int KS, int WR, int D>
+static bool launch_strip_cfg(const dvie_conv_desc& p, hipStream_t s) {
+  if (p.out_f32) {
+    launch_strip_k<KS, WR, D, -1>(p, s);
+    return true;
+  }
+  switch ((p.res ? 1 : 0) | (p.beta ? 2 : 0) | (p.dact ? 4 : 0)) {
+    case 0: launch_strip_k<KS, WR, D, 0>(p, s); return true;
+    case 1: launch_strip_k<KS, WR, D, 1>(p, s); return true;
+    case 2: launch_strip_k<KS, WR, D, 2>(p, s); return true;
+    case 3: launch_strip_k<KS, WR, D, 3>(p, s); return true;
+    case 4: launch_strip_k<KS, WR, D, 4>(p, s); return true;
+    case 5: launch_strip_k<KS, WR, D, 5>(p, s); return true;
+    case 6: launch_strip_k<KS, WR, D, 6>(p, s); return true;
+  }
+  return false;
+}
+
+// DVIE_CONV_STRIP: 0 = conv_ws_kernel (A/B runs); 1 = strip, 4 rows per iteration, 2
+// iterations ahead (one 8-wave workgroup per CU); 2 (default) = strip, 2 rows, 2 ahead (two
+// 4-wave workgroups per CU); 3 = strip, 2 rows, 1 ahead.  Read per launch (tuning sweeps).
+// Measured (tools/conv_strip_micro.py, profiles/r02_ab/conv_strip_micro.txt), 8x256x512
+// 64->64: tile kernel / mode 2 = 96 / 96 us plain, 138 / 108 residual, 130 / 111 activation
+// input, 159 / 130 accumulate + activation input.
+static int strip_mode() {
+  const char* e = getenv("DVIE_CONV_STRIP");
+  return e && *e ? atoi(e) : 2;
+}
+
+template <int KS>
+static bool launch_strip(const dvie_conv_desc& p, hipStream_t s) {
+  switch (strip_mode()) {
+    case 1: return launch_strip_cfg<KS, 4, 2>(p, s);
+    case 2: return launch_strip_cfg<KS, 2, 2>(p, s);
+    case 3: return launch_strip_cfg<KS, 2, 1>(p, s);
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------------------
 // Dense-K variant for 3x3 stride-1 convs with few input channels (c = 8, 16 or 24: the data
 // gradients of the 3- / 20-channel output heads into their 448-channel hidden layers, the
 // 20-channel seg encoder, the image stems).  The chunked kernels give every tap a 64-channel
@@ -989,10 +1284,10 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (t3 && p.c <= 64 && p.cout <= 64 && (cfg == -3 || cfg == 8) && (long long)p.n * p.oh * p.ow >= 65536) {
     // single input chunk, one 64-channel output tile: weights stay in VGPRs
     switch ((p.c + 15) / 16) {
-      case 1: launch_ws<1>(p, s); break;
-      case 2: launch_ws<2>(p, s); break;
-      case 3: launch_ws<3>(p, s); break;
-      default: launch_ws<4>(p, s); break;
+      case 1: if (!launch_strip<1>(p, s)) launch_ws<1>(p, s); break;
+      case 2: if (!launch_strip<2>(p, s)) launch_ws<2>(p, s); break;
+      case 3: if (!launch_strip<3>(p, s)) launch_ws<3>(p, s); break;
+      default: if (!launch_strip<4>(p, s)) launch_ws<4>(p, s); break;
     }
     return true;
   }

@@ -36,9 +36,7 @@ def _lrelu(v):
     return torch.where(v > 0, v, 0.2 * v)
 
 
-@pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("shape", SHAPES)
-def test_conv_epilogue_operands(dev, shape, mode):
+def _run(dev, shape, mode, out_f32=False):
     n, H, W, c, cout, k = shape
     g = torch.Generator().manual_seed(7)
     x = _bf(torch.randn(n, H, W, c, generator=g))
@@ -63,11 +61,12 @@ def test_conv_epilogue_operands(dev, shape, mode):
     kpad = (K + 63) // 64 * 64
     wp = torch.zeros(cout, kpad)
     wp[:, :K] = wt.permute(0, 2, 3, 1).reshape(cout, K)  # [co][tap * c + ci]
+    odt = torch.float32 if out_f32 else torch.bfloat16  # output (and residual) dtype
     xd = x.to(torch.bfloat16).to(dev)
     wd = wp.to(torch.bfloat16).to(dev)
     bd = bias.to(dev)
-    yd = (yold if yold is not None else torch.zeros(n, H, W, cout)).to(torch.bfloat16).to(dev)
-    rd = res.to(torch.bfloat16).to(dev) if res is not None else None
+    yd = (yold if yold is not None else torch.zeros(n, H, W, cout)).to(odt).to(dev)
+    rd = res.to(odt).to(dev) if res is not None else None
     zd = z.to(torch.bfloat16).to(dev) if z is not None else None
 
     d = L.ConvDesc()
@@ -80,10 +79,42 @@ def test_conv_epilogue_operands(dev, shape, mode):
     d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = k, k, -(k // 2), -(k // 2), 1, 1
     d.yh, d.yw, d.osy, d.osx, d.ory, d.orx = H, W, 1, 1, 0, 0
     d.act, d.dact, d.beta = act, L.ACT_LRELU if z is not None else L.ACT_NONE, int(yold is not None)
-    d.dtype, d.out_f32, d.alpha = L.BF16, 0, 0.2
+    d.dtype, d.out_f32, d.alpha = L.BF16, int(out_f32), 0.2
     L.check(L.load().dvie_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
             "conv")
     torch.cuda.synchronize()
     out = yd.float().cpu()
-    err = float((out - ref).abs().max() / ref.abs().max())
+    return float((out - ref).abs().max() / ref.abs().max())
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_epilogue_operands(dev, shape, mode):
+    err = _run(dev, shape, mode)
     assert err < 1e-2, (shape, mode, err)
+
+
+STRIP_SHAPES = [  # 3x3, c and cout <= 64, >= 65536 output pixels: the weight-stationary family
+    (2, 131, 250, 64, 64, 3),   # ragged rows (not a multiple of the iteration rows) and columns
+    (1, 260, 270, 48, 40, 3),   # 3 K slices, 40 output channels (a partial 32-channel block)
+    (8, 20, 2600, 32, 32, 3),   # more strips than resident workgroups: one segment per strip
+]
+
+
+@pytest.mark.parametrize("strip", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", STRIP_SHAPES)
+def test_conv_strip_modes(dev, shape, mode, strip, monkeypatch):
+    """Strip kernel (DVIE_CONV_STRIP 1-3: rows per iteration / look-ahead) vs the tile kernel
+    (0), every epilogue-operand set, bf16 output."""
+    monkeypatch.setenv("DVIE_CONV_STRIP", strip)
+    err = _run(dev, shape, mode)
+    assert err < 1e-2, (shape, mode, strip, err)
+
+
+@pytest.mark.parametrize("mode", ["none", "res+beta+z"])
+@pytest.mark.parametrize("strip", ["0", "1"])
+def test_conv_strip_fp32_out(dev, mode, strip, monkeypatch):
+    monkeypatch.setenv("DVIE_CONV_STRIP", strip)
+    err = _run(dev, (2, 131, 250, 64, 64, 3), mode, out_f32=True)
+    assert err < 1e-2, (mode, strip, err)
