@@ -32,7 +32,8 @@ KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwis
               8: "batchnorm_fwd", 9: "batchnorm_bwd", 10: "head_fwd", 11: "head_bwd"}
 # HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
 # this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01zc_pmc", "traffic.json")
+PMC_DIR = "r02j_pmc"  # tools/pmc_bench.sh on the current tree
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", PMC_DIR, "traffic.json")
 
 
 
@@ -297,20 +298,29 @@ def main():
         fl = sum(r["flops"] for r in conv)
         by = sum(r["bytes"] for r in conv)
         tf = fl / (ms * 1e-3) / 1e12
-        traffic = None
+        traffic = wg_traffic = None
         if os.path.exists(PMC_TRAFFIC):
-            t = json.load(open(PMC_TRAFFIC)).get("conv")
+            pm = json.load(open(PMC_TRAFFIC))
+            t, tw = pm.get("conv"), pm.get("wgrad")
             traffic = round(t["bytes_per_launch"]) if t else None
+            wg_traffic = round(tw["bytes_per_launch"]) if tw else None
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                 "traffic": traffic, "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE, "
-                                                     "profiles/r01zc_pmc)",
+                                                     f"profiles/{PMC_DIR})",
                 "algorithmic_bytes_per_launch": round(by / max(1, n)),
-                "kernel": "conv fwd+dgrad family (conv_halo / conv_ws / conv1x1 / conv_igemm kernels)",
+                "kernel": "conv fwd+dgrad family (conv_halo / conv_strip / conv_nk / conv1x1 / conv_igemm kernels)",
                 "launches_per_step": n // max(1, a.profile_steps),
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
                 "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4),
                 # sum over launches of max(F/P_mfma, B/BW_hbm) over measured time
                 "per_op_roofline_time_frac": round(sum(r["roof_ms"] for r in conv) / ms, 4)}
+        wg = agg.get("conv_wgrad")
+        if wg:  # weight gradients: algorithmic bytes (x, dy read once, dW written) vs PMC traffic
+            roof["wgrad"] = {"launches_per_step": wg["n"] // max(1, a.profile_steps),
+                             "avg_launch_us": round(wg["ms"] * 1e3 / max(1, wg["n"]), 2),
+                             "tflops": round(wg["flops"] / (wg["ms"] * 1e-3) / 1e12, 2),
+                             "algorithmic_bytes_per_launch": round(wg["bytes"] / max(1, wg["n"])),
+                             "traffic": wg_traffic}
     if a.ops_out and rank == 0:
         with open(a.ops_out, "w") as f:
             f.write(f"{'class':12s} {'layer':42s} {'n':>3s} {'ms':>8s} {'TFLOP/s':>8s} {'GB/s':>8s} {'roof%':>6s}\n")

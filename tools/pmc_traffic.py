@@ -11,8 +11,8 @@ import json
 import re
 import sys
 
-FAM = [("conv", r"conv_halo_kernel|conv_ws_kernel|conv1x1_kernel|conv_igemm_kernel"),
-       ("wgrad", r"wgrad_halo_kernel|wgrad_kernel")]
+FAM = [("conv", r"conv_halo_kernel|conv_ws_kernel|conv_strip_kernel|conv_nk_kernel|conv1x1_kernel|conv_igemm_kernel"),
+       ("wgrad", r"wgrad_halo_kernel|wgrad_kernel|wgrad_wide_kernel")]
 
 
 def family(name):
