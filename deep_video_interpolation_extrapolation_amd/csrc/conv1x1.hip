@@ -89,7 +89,10 @@ struct G1Cfg {
   static __device__ __forceinline__ int swz(int row) { return NCH == 8 ? (row >> 1) & 7 : (row >> 2) & 3; }
 };
 
-template <int TMC, int NS, int KC, int NWP, int MI, int NWC, bool OUTF32>
+// PRE (bf16 output, single K-step only): epilogue operands loaded into registers right after
+// the stage's DMA, so their HBM latency overlaps the operand DMA instead of following the
+// MFMAs (1 residual, 2 accumulate target, 4 activation input).
+template <int TMC, int NS, int KC, int NWP, int MI, int NWC, bool OUTF32, int PRE = 0>
 __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv_desc p, int n_ct, int n_tiles) {
   typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
   constexpr int NW = C::NW;
@@ -182,6 +185,31 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
 #pragma unroll
   for (int k = 0; k < (NS > 1 ? NS - 1 : 1); ++k)
     if (k < nk) stage(k, k);
+
+  // epilogue-operand prefetch (PRE): lane (pixel wp*32*MI + 32*i + r32, channels
+  // c0 + wc*32*TMC + 32*j + 16*P + 8*h .. +7); identity output placement only (checked at launch)
+  static_assert(PRE == 0 || (NS == 1 && !OUTF32), "operand prefetch: single K-step, bf16 output");
+  i32x4 pr_r[(PRE & 1) ? MI : 1][TMC][2], pr_b[(PRE & 2) ? MI : 1][TMC][2], pr_z[(PRE & 4) ? MI : 1][TMC][2];
+  if constexpr (PRE != 0) {
+    const int wp0 = wave % NWP, wc0 = wave / NWP;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < TMC; ++j)
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          const int pix = p0 + wp0 * 32 * MI + 32 * i + r32;
+          const int co = c0 + wc0 * 32 * TMC + 32 * j + 16 * P + 8 * hh;
+          const bool ok = pix < npix && co < p.cout;
+          const long long q = ok ? pix : 0;
+          if constexpr ((PRE & 1) != 0)
+            pr_r[i][j][P] = ok ? *(const i32x4*)((const bf16_t*)p.res + q * p.res_ld + co) : i32x4{0, 0, 0, 0};
+          if constexpr ((PRE & 2) != 0)
+            pr_b[i][j][P] = ok ? *(const i32x4*)((const bf16_t*)p.y + q * p.y_ld + co) : i32x4{0, 0, 0, 0};
+          if constexpr ((PRE & 4) != 0)
+            pr_z[i][j][P] = ok ? *(const i32x4*)((const bf16_t*)p.z + q * p.z_ld + co) : i32x4{0, 0, 0, 0};
+        }
+  }
   for (int k = 0; k < nk; ++k) {
     const int sb = k % NS;
     // stage k has landed for every wave: this wave's own pieces by the counted wait (stage
@@ -296,18 +324,27 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
         bf16_t* dst = (bf16_t*)p.y + yp * p.y_ld + co;
         float t[8];
         if (p.res) {
-          unpack8(*(const i32x4*)((const bf16_t*)p.res + yp * p.res_ld + co), t);
+          if constexpr ((PRE & 1) != 0)
+            unpack8(pr_r[(PRE & 1) ? i : 0][j][P], t);
+          else
+            unpack8(*(const i32x4*)((const bf16_t*)p.res + yp * p.res_ld + co), t);
 #pragma unroll
           for (int e = 0; e < 8; ++e) w[e] += t[e];
         }
         if (p.beta) {
-          unpack8(*(const i32x4*)dst, t);
+          if constexpr ((PRE & 2) != 0)
+            unpack8(pr_b[(PRE & 2) ? i : 0][j][P], t);
+          else
+            unpack8(*(const i32x4*)dst, t);
 #pragma unroll
           for (int e = 0; e < 8; ++e) w[e] += t[e];
         }
         act1(w, p.act, p.alpha);
         if (p.dact) {
-          unpack8(*(const i32x4*)((const bf16_t*)p.z + yp * p.z_ld + co), t);
+          if constexpr ((PRE & 4) != 0)
+            unpack8(pr_z[(PRE & 4) ? i : 0][j][P], t);
+          else
+            unpack8(*(const i32x4*)((const bf16_t*)p.z + yp * p.z_ld + co), t);
           dact1(w, t, p.dact, p.alpha);
         }
         i32x4 o;
@@ -319,6 +356,19 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
   }
 }
 
+// operand sets instantiated per tile shape: single K-step, at most 4 accumulators per wave
+// (a single prefetched operand on the 8-accumulator 64->256 tile measured no gain)
+template <int V, int NS, int MT>
+struct PreOk {
+  static constexpr int v = NS != 1 || MT > 4 ? 0 : V;
+};
+
+// DVIE_1X1_PRE=0: no epilogue-operand prefetch (A/B runs); read per launch
+static bool pre_env_on() {
+  const char* e = getenv("DVIE_1X1_PRE");
+  return !(e && *e == '0');
+}
+
 template <int TMC, int NS, int KC = 64, int NWP = 8, int MI = 1, int NWC = 1>
 static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
@@ -326,10 +376,31 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   const int npix = p.n * p.oh * p.ow;
   const int n_ct = (p.cout + C::BC - 1) / C::BC;
   const int n_tiles = n_ct * ((npix + C::BP - 1) / C::BP);
-  if (p.out_f32)
+  if (p.out_f32) {
     hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, true>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
-  else
-    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
+    return;
+  }
+  // single K-step with identity placement: prefetch the epilogue operands (all of them when
+  // the registers allow -- MI * TMC <= 4 -- else the activation input, or the residual)
+  const bool ident = p.osy == 1 && p.osx == 1 && p.ory == 0 && p.orx == 0 && p.yh == p.oh && p.yw == p.ow;
+  int pre = 0;
+  if constexpr (NS == 1) {
+    if (ident && p.c <= KC && pre_env_on()) {
+      pre = MI * TMC > 4 ? 0 : (p.res ? 1 : 0) | (p.beta ? 2 : 0) | (p.dact ? 4 : 0);
+    }
+  }
+  switch (pre) {
+#define DVIE_1X1_PRE_CASE(V)                                                                                      \
+  case V:                                                                                                        \
+    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false, PreOk<V, NS, MI * TMC>::v>), dim3(n_tiles), \
+                       dim3(64 * NW), 0, s, p, n_ct, n_tiles);                                                   \
+    break;
+    DVIE_1X1_PRE_CASE(1) DVIE_1X1_PRE_CASE(2) DVIE_1X1_PRE_CASE(3) DVIE_1X1_PRE_CASE(4) DVIE_1X1_PRE_CASE(5)
+    DVIE_1X1_PRE_CASE(6) DVIE_1X1_PRE_CASE(7)
+#undef DVIE_1X1_PRE_CASE
+    default:
+      hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
+  }
 }
 
 // Returns true when the 1x1 GEMM kernel took the launch.
@@ -348,7 +419,10 @@ bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
   // at 8x256x512, tools/conv_tune.py)
   // (DVIE_CONV1X1_WIDE overrides the wide-layer choice alone, for A/B runs of the whole step)
   static const int wide = getenv("DVIE_CONV1X1_WIDE") && *getenv("DVIE_CONV1X1_WIDE") ? atoi(getenv("DVIE_CONV1X1_WIDE")) : 116;
-  if (cfg < 0) cfg = cout <= 64 ? 100 : cout <= 128 ? 101 : wide;
+  // single K-step, 65-128 output channels: two 64-channel column tiles with every epilogue
+  // operand prefetched beat one 128-channel tile (8x128x256 64->128: 33 vs 35 us residual,
+  // 48 vs 56 us accumulate + activation input, tools/conv_epi_micro.py)
+  if (cfg < 0) cfg = cout <= 64 ? 100 : cout <= 128 ? (one ? 100 : 101) : wide;
   switch (cfg) {
     case 100: one ? launch_1x1<2, 1>(p, s) : launch_1x1<2, 3>(p, s); break;
     case 101: one ? launch_1x1<4, 1>(p, s) : launch_1x1<4, 3>(p, s); break;

@@ -24,6 +24,9 @@ SHAPES = [  # n, H, W, c, cout, k
     (2, 35, 90, 256, 64, 3),    # halo 64-channel tiles, 4 chunks
     (2, 40, 70, 16, 64, 3),     # dense-K
     (2, 37, 77, 128, 256, 1),   # 1x1
+    (2, 37, 77, 64, 256, 1),    # 1x1 single K-step, 64-pixel x 128-channel wave tiles: one operand prefetched
+    (2, 37, 77, 64, 64, 1),     # 1x1 single K-step, every operand prefetched
+    (2, 37, 77, 48, 128, 1),    # 1x1 single K-step, 48 input channels (zero-padded K)
 ]
 MODES = ["none", "res", "beta", "z", "res+z", "beta+z", "res+beta+z"]
 
