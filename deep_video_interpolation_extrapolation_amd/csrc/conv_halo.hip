@@ -140,6 +140,8 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   const int wc = wave / WP, wp = wave % WP;
   const int r32 = lane & 31, hh = lane >> 5;
   const int nchunks = (p.c + 63) >> 6;  // c < 64: one zero-padded chunk
+  // epi_pre bit 1: static priority for the second-dispatched half of the waves (DVIE_SETPRIO)
+  if ((epi_pre & 2) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const unsigned OOB = 0xFFFFFFF0u;
 
   // ---- tiles of this workgroup: one (remapped) tile, or an XCD-local strided range ----
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   // Buffer loads from a per-tile base: every wave issues the same count (lanes outside the
   // output get an out-of-range offset and load zeros), so the step's vmcnt stays exact.
   constexpr int PRE_T = C::NT >= 2 ? C::NT - 2 : 0;
-  const bool PRE = !OUTF32 && epi_pre;
+  const bool PRE = !OUTF32 && (epi_pre & 1);
   const int npre = PRE ? TM * 4 * ((p.res ? 1 : 0) + (p.beta ? 1 : 0) + (p.dact ? 1 : 0)) : 0;
   i32x4 pre_r[TM][2][2], pre_b[TM][2][2], pre_z[TM][2][2];
   auto epi_prefetch = [&](const JobInfo& Jt) {
@@ -488,6 +490,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
 
 // DVIE_EPI_PREFETCH=0: epilogue operands loaded in the epilogue (A/B runs)
 static const bool epi_prefetch_on = !(getenv("DVIE_EPI_PREFETCH") && *getenv("DVIE_EPI_PREFETCH") == '0');
+static const int halo_setprio = getenv("DVIE_SETPRIO") && *getenv("DVIE_SETPRIO") == '1' ? 2 : 0;
 
 template <int TM, int WC, int WP, int TH, int TW>
 static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
@@ -506,10 +509,10 @@ static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
     const int grid = persistent ? cap : n_tiles;
     if (p.out_f32)
       hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
-                         n_tiles, tiles_x, tiles_y, persistent, 0);
+                         n_tiles, tiles_x, tiles_y, persistent, halo_setprio);
     else
       hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, false>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
-                         n_tiles, tiles_x, tiles_y, persistent, epi_prefetch_on ? 1 : 0);
+                         n_tiles, tiles_x, tiles_y, persistent, (epi_prefetch_on ? 1 : 0) | halo_setprio);
     return true;
   }
 }
