@@ -356,12 +356,213 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
   }
 }
 
+// Persistent form for multi-K-step layers (bf16 output): a workgroup walks tiles T = b,
+// b + G, ... (b its XCD-contiguous id) and the stage ring runs across tile boundaries, so the
+// first K-steps of the next tile are in flight while this tile finishes its MFMAs and its
+// epilogue (the one-tile-per-workgroup form pays a stage latency at every tile start).
+template <int TMC, int NS, int KC, int NWP, int MI, int NWC>
+__global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_persist_kernel(const dvie_conv_desc p, int n_ct, int n_tiles) {
+  typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
+  constexpr int NW = C::NW;
+  static_assert(NS >= 2, "stage ring");
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  const int G = gridDim.x;
+  const int g = blockIdx.x & 7, i8 = blockIdx.x >> 3;
+  const int q8 = G >> 3, r8 = G & 7;
+  const int b = (g < r8 ? g * (q8 + 1) : r8 * (q8 + 1) + (g - r8) * q8) + i8;
+  const int npix = p.n * p.oh * p.ow;
+  const int nk = (p.c + KC - 1) / KC;
+  const int my_tiles = b < n_tiles ? (n_tiles - 1 - b) / G + 1 : 0;
+  const int njobs = my_tiles * nk;
+  if (njobs == 0) return;
+
+  const int lrow = lane / C::NCH, lch = lane % C::NCH;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const unsigned wbytes = (unsigned)p.cout * (unsigned)p.kpad * 2u;
+
+  // job jj = (tile i = jj / nk of this workgroup, K-step k = jj % nk) into stage sb
+  auto stage = [&](int jj, int sb) {
+    const int i = jj / nk, k = jj - nk * (jj / nk);
+    const int T = b + i * G;
+    const int c0 = (T % n_ct) * C::BC, p0 = (T / n_ct) * C::BP;
+    char* X = smem + sb * C::STAGE;
+    char* W = X + C::XSZ;
+    const int xr = (int)(xbytes - (unsigned long long)k * C::RB);
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)k * C::RB), 0, xr, 0x00020000);
+    const unsigned wb = (unsigned)(c0 * p.kpad + KC * k) * 2u;
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + wb), 0, (int)(wbytes - wb), 0x00020000);
+    const int cvalid = p.c - KC * k;
+#pragma unroll
+    for (int q = 0; q < C::XQ; ++q) {
+      const int row = (wave + NW * q) * C::RPP + lrow;
+      const int cs = lch ^ C::swz(row);
+      const unsigned o = (cs * 8 < cvalid && p0 + row < npix) ? (unsigned)(p0 + row) * (unsigned)p.x_ld * 2u + cs * 16u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_1x1)(X + (wave + NW * q) * 1024), 16, o, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < C::WQ; ++q) {
+      if (wave + NW * q < C::BC / C::RPP) {
+        const int row = (wave + NW * q) * C::RPP + lrow;
+        const int cs = lch ^ C::swz(row);
+        const unsigned o = (row < C::BC && cs * 8 < cvalid) ? (unsigned)row * (unsigned)p.kpad * 2u + cs * 16u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_1x1)(W + (wave + NW * q) * 1024), 16, o, 0, 0, 0);
+      }
+    }
+  };
+
+  const int wp = wave % NWP, wc = wave / NWP;
+  int xf[C::NSL], wf[C::NSL];
+#pragma unroll
+  for (int sl = 0; sl < C::NSL; ++sl) {
+    const int prow = wp * 32 * MI + r32;
+    xf[sl] = prow * C::RB + (((2 * sl + hh) ^ C::swz(prow)) << 4);
+    wf[sl] = (wc * 32 * TMC + r32) * C::RB + (((2 * sl + hh) ^ C::swz(r32)) << 4);
+  }
+
+  // leave the stages issued after job j (at most NS-2, fewer at the end) in flight
+  constexpr int P_HI = C::XQ + C::WQ, P_LO = C::XQ + C::WQ - 1;  // pieces per wave per stage
+  static_assert((NS - 2) * P_HI < 64, "vmcnt is 6 bits");
+  const bool hi = wave + NW * (C::WQ - 1) < C::BC / C::RPP;
+  auto wait_stages = [&](int j) {
+    const int m = min(NS - 2, njobs - 1 - j);
+    if (m >= 3) {
+      if (hi) DVIE_VMCNT1(3 * P_HI); else DVIE_VMCNT1(3 * P_LO);
+    } else if (m == 2) {
+      if (hi) DVIE_VMCNT1(2 * P_HI); else DVIE_VMCNT1(2 * P_LO);
+    } else if (m == 1) {
+      if (hi) DVIE_VMCNT1(P_HI); else DVIE_VMCNT1(P_LO);
+    } else {
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+  };
+
+  f32x16 acc[MI][TMC];
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < njobs) stage(k, k);
+  for (int jj = 0; jj < njobs; ++jj) {
+    const int k = jj - nk * (jj / nk);
+    if (k == 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < TMC; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    }
+    // job jj landed: this wave's pieces by a counted wait (stages issued after it may stay in
+    // flight), other waves' by the barrier.  After an epilogue the wait was done before its
+    // stores (so that they never have to drain here).
+    if (k != 0 || jj == 0) wait_stages(jj);
+    __builtin_amdgcn_s_barrier();
+    if (jj + NS - 1 < njobs) stage(jj + NS - 1, (jj + NS - 1) % NS);
+    const char* X = smem + (jj % NS) * C::STAGE;
+    const char* W = X + C::XSZ;
+#pragma unroll
+    for (int sl = 0; sl < C::NSL; ++sl) {
+      i32x4 bq[MI], a[TMC];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) bq[i] = *(const i32x4*)(X + xf[sl] + i * 32 * C::RB);
+#pragma unroll
+      for (int j = 0; j < TMC; ++j) a[j] = *(const i32x4*)(W + wf[sl] + j * 32 * C::RB);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < TMC; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[j]),
+                                                              __builtin_bit_cast(bf16x8, bq[i]), acc[i][j], 0, 0, 0);
+    }
+    if (k + 1 < nk) continue;
+    if (jj + 1 < njobs) wait_stages(jj + 1);
+
+    // ---- epilogue of tile T (as conv1x1_kernel, bf16 output)
+    const int T = b + (jj / nk) * G;
+    const int c0 = (T % n_ct) * C::BC, p0 = (T / n_ct) * C::BP;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int pix = p0 + wp * 32 * MI + 32 * i + r32;
+      float v[TMC][2][8];
+#pragma unroll
+      for (int j = 0; j < TMC; ++j)
+#pragma unroll
+        for (int P = 0; P < 2; ++P)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * P + e]),
+                                                             __float_as_uint(acc[i][j][8 * P + 4 + e]), false, false);
+            v[j][P][e] = __uint_as_float(sw[0]);
+            v[j][P][4 + e] = __uint_as_float(sw[1]);
+          }
+      if (pix >= npix) continue;
+      long long yp = pix;
+      if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) {
+        const int hw = p.oh * p.ow;
+        const int n = pix / hw, r = pix - n * hw;
+        const int oy = r / p.ow, ox = r - oy * p.ow;
+        yp = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+      }
+#pragma unroll
+      for (int j = 0; j < TMC; ++j)
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          const int co = c0 + wc * 32 * TMC + 32 * j + 16 * P + 8 * hh;
+          if (co >= p.cout) continue;
+          float* w = v[j][P];
+          if (p.bias) {
+            const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[e] += b0[e];
+              w[4 + e] += b1[e];
+            }
+          }
+          bf16_t* dst = (bf16_t*)p.y + yp * p.y_ld + co;
+          float t[8];
+          if (p.res) {
+            unpack8(*(const i32x4*)((const bf16_t*)p.res + yp * p.res_ld + co), t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] += t[e];
+          }
+          if (p.beta) {
+            unpack8(*(const i32x4*)dst, t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] += t[e];
+          }
+          act1(w, p.act, p.alpha);
+          if (p.dact) {
+            unpack8(*(const i32x4*)((const bf16_t*)p.z + yp * p.z_ld + co), t);
+            dact1(w, t, p.dact, p.alpha);
+          }
+          i32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (int)pk_bf16(w[2 * e], w[2 * e + 1]);
+          *(i32x4*)dst = o;
+        }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 // operand sets instantiated per tile shape: single K-step, at most 4 accumulators per wave
 // (a single prefetched operand on the 8-accumulator 64->256 tile measured no gain)
 template <int V, int NS, int MT>
 struct PreOk {
   static constexpr int v = NS != 1 || MT > 4 ? 0 : V;
 };
+
+// DVIE_1X1_PERSIST=0: one tile per workgroup for multi-K-step layers (A/B runs); read per launch
+static bool persist_env_on() {
+  const char* e = getenv("DVIE_1X1_PERSIST");
+  return !(e && *e == '0');
+}
 
 // DVIE_1X1_PRE=0: no epilogue-operand prefetch (A/B runs); read per launch
 static bool pre_env_on() {
@@ -379,6 +580,18 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   if (p.out_f32) {
     hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, true>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
     return;
+  }
+  if constexpr (NS >= 2 && NS <= 5 && MI * TMC <= 4) {
+    // several K-steps and more tiles than resident workgroups: persistent stage ring
+    // (8x256x512 256->64: 142 -> 127 us, 8x128x256 256->128: 47 -> 41 us; the 8-accumulator
+    // wide tiles of the heads measured no gain, 896->448 +3%: they keep one tile per workgroup)
+    const int per_cu = 163840 / C::SMEM;
+    const int G = 256 * (per_cu > 2 ? 2 : per_cu);
+    if (persist_env_on() && p.c > KC && n_tiles > G) {
+      hipLaunchKernelGGL((conv1x1_persist_kernel<TMC, NS, KC, NWP, MI, NWC>), dim3(G), dim3(64 * NW), 0, s, p, n_ct,
+                         n_tiles);
+      return;
+    }
   }
   // single K-step with identity placement: prefetch the epilogue operands (all of them when
   // the registers allow -- MI * TMC <= 4 -- else the activation input, or the residual)

@@ -27,6 +27,9 @@ SHAPES = [  # n, H, W, c, cout, k
     (2, 37, 77, 64, 256, 1),    # 1x1 single K-step, 64-pixel x 128-channel wave tiles: one operand prefetched
     (2, 37, 77, 64, 64, 1),     # 1x1 single K-step, every operand prefetched
     (2, 37, 77, 48, 128, 1),    # 1x1 single K-step, 48 input channels (zero-padded K)
+    (4, 128, 160, 128, 256, 1),  # 1x1 several K-steps, more tiles than resident workgroups: persistent
+    (4, 128, 160, 256, 64, 1),   # the same, 64-channel tiles (3-stage ring)
+    (3, 131, 177, 192, 96, 1),   # the same, ragged pixel count, partial 128-channel tile
 ]
 MODES = ["none", "res", "beta", "z", "res+z", "beta+z", "res+beta+z"]
 
