@@ -714,6 +714,14 @@ class Plan:
         d.res, d.res_ld, d.z, d.z_ld = res, res_ld, z, z_ld
         d.act, d.dact, d.beta, d.dtype = act, dact, beta, self.dt
         d.alpha, d.scale = 0.2, scale
+        # profiling meta: algorithmic bytes = output written once (+ read when accumulating),
+        # residual / activation input read once, each source read once at its own resolution
+        npx = n * h * w
+        nbytes = self.es * c * (npx * (1 + int(bool(beta)) + int(res is not None) + int(z is not None))
+                                + sum(n * sh * sw for (_, _, sh, sw) in srcs))
+        o.meta = dict(cls="pointwise", name=f"ew{op} {n}x{h}x{w}x{c} src{len(srcs)}"
+                      + ("+res" if res is not None else "") + ("+acc" if beta else "") + ("+z" if z is not None else ""),
+                      flops=0.0, bytes=float(nbytes))
         return o
 
     def _part(self, part):
