@@ -1,0 +1,83 @@
+"""Pointwise multi-resolution ops through the C ABI (dvie_ew) against torch on the same
+bf16-rounded operands: EW_FUSE (bilinear upsample of up to three sources, summed, LeakyReLU)
+vs F.interpolate (nets/HRNet.py:219-222,577-580), and EW_UPT (the gather-form adjoint of that
+upsample) vs autograd through F.interpolate, for 2x / 4x / 8x ratios, both align_corners
+modes, ragged sizes and channel slices of wider buffers.  fp32 accumulation in both, bf16
+output rounding: tolerance 1e-2 relative to max |y|."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deep_video_interpolation_extrapolation_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _run(d):
+    L.check(L.load().dvie_ew(ctypes.byref(d), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "ew")
+    torch.cuda.synchronize()
+
+
+def _desc(op, n, h, w, c, y, y_ld):
+    d = L.EwDesc()
+    d.op, d.n, d.h, d.w, d.c = op, n, h, w, c
+    d.y, d.y_ld = y.data_ptr(), y_ld
+    d.dtype, d.alpha, d.scale = L.BF16, 0.2, 1.0
+    return d
+
+
+# (n, fine h, fine w, coarse h, coarse w, c, align)
+CASES = [(2, 64, 128, 16, 32, 64, 0), (2, 64, 128, 32, 64, 32, 0), (1, 77, 130, 10, 17, 16, 0),
+         (2, 64, 128, 16, 32, 64, 1), (1, 40, 72, 20, 36, 24, 1), (1, 96, 64, 12, 8, 8, 0)]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_upsample_adjoint(dev, case):
+    n, H, W, h, w, c, align = case
+    g = torch.Generator().manual_seed(3)
+    gy = _bf(torch.randn(n, H, W, c, generator=g))
+    x = torch.zeros(n, c, h, w, requires_grad=True)
+    F.interpolate(x, size=(H, W), mode="bilinear", align_corners=bool(align)).backward(gy.permute(0, 3, 1, 2))
+    ref = x.grad.permute(0, 2, 3, 1)
+    # output into a channel slice of a wider buffer, source from one
+    yb = torch.zeros(n, h, w, c + 16, dtype=torch.bfloat16, device=dev)
+    sb = torch.zeros(n, H, W, c + 8, dtype=torch.bfloat16, device=dev)
+    sb[..., 8:] = gy.to(torch.bfloat16)
+    d = _desc(L.EW_UPT, n, h, w, c, yb[..., 16:], c + 16)
+    d.nsrc, d.src0, d.src_ld0, d.sh0, d.sw0, d.align = 1, sb[..., 8:].data_ptr(), c + 8, H, W, align
+    _run(d)
+    out = yb[..., 16:].float().cpu()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2, (case, err)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fuse_upsample(dev, case):
+    n, H, W, h, w, c, align = case
+    g = torch.Generator().manual_seed(5)
+    x0 = _bf(torch.randn(n, H, W, c, generator=g))
+    x1 = _bf(torch.randn(n, h, w, c, generator=g))
+    x2 = _bf(torch.randn(n, max(1, h // 2), max(1, w // 2), c, generator=g))
+    ref = x0.clone()
+    for s in (x1, x2):
+        ref = ref + F.interpolate(s.permute(0, 3, 1, 2), size=(H, W), mode="bilinear",
+                                  align_corners=bool(align)).permute(0, 2, 3, 1)
+    ref = torch.where(ref > 0, ref, 0.2 * ref)
+    y = torch.zeros(n, H, W, c, dtype=torch.bfloat16, device=dev)
+    srcs = [t.to(torch.bfloat16).to(dev) for t in (x0, x1, x2)]
+    d = _desc(L.EW_FUSE, n, H, W, c, y, c)
+    d.nsrc, d.align, d.act = 3, align, L.ACT_LRELU
+    for i, t in enumerate(srcs):
+        setattr(d, f"src{i}", t.data_ptr())
+        setattr(d, f"src_ld{i}", c)
+        setattr(d, f"sh{i}", t.shape[1])
+        setattr(d, f"sw{i}", t.shape[2])
+    _run(d)
+    err = float((y.float().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2, (case, err)
