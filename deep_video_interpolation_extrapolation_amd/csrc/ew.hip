@@ -100,6 +100,43 @@ __device__ __forceinline__ float upt_weight(int f, int cidx, int cs, int fs, int
   return wgt;
 }
 
+// Upsample adjoint for an integer ratio R (align_corners False): the fine rows / columns whose
+// stencil can reach coarse index i are R*i - R/2 - 1 .. R*i + R + R/2 (2R + 2 candidates, one
+// spare on each side).  Row weights are uniform over a block (one coarse row), so zero rows
+// are skipped by a uniform branch; within a row every candidate column is loaded
+// unconditionally (clamped address, zero weight outside), so the 2R + 2 loads of a row issue
+// back to back instead of one per divergent branch.  Weights: the forward's own lerp.
+template <typename T, int VW, int R>
+__device__ __forceinline__ void upt_ratio(float* v, const T* __restrict__ s, long long ld, int n, int y, int x, int c,
+                                          int h, int w, int sh, int sw) {
+  constexpr int NC = 2 * R + 2;
+  const int Y0 = R * y - R / 2 - 1, X0 = R * x - R / 2 - 1;
+  float wx[NC];
+  int xo[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int X = X0 + j;
+    const bool in = X >= 0 && X < sw;
+    wx[j] = in ? upt_weight(X, x, w, sw, 0) : 0.f;
+    xo[j] = in ? X : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int Y = Y0 + i;
+    if (Y < 0 || Y >= sh) continue;
+    const float wy = upt_weight(Y, y, h, sh, 0);
+    if (wy == 0.f) continue;
+    const T* srow = s + ((long long)n * sh + Y) * sw * ld + c;
+    float t[NC][VW];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) VecN<T, VW>::load(srow + (long long)xo[j] * ld, t[j]);
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] += wy * wx[j] * t[j][k];
+  }
+}
+
 // One thread = VW channels of one pixel; blockIdx.y = image row (n, y), so the per-element
 // index math is one 32-bit division by the channel-vector count.
 template <typename T, int VW>
@@ -125,6 +162,14 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
     case DVIE_EW_UPT: {
       // coarse output (y, x) of a (h, w) grid, fine source (sh0, sw0)
       const T* s = (const T*)p.src0;
+      if (!p.align && p.sh0 == 2 * p.h && p.sw0 == 2 * p.w) {
+        upt_ratio<T, VW, 2>(v, s, p.src_ld0, n, y, x, c, p.h, p.w, p.sh0, p.sw0);
+        break;
+      }
+      if (!p.align && p.sh0 == 4 * p.h && p.sw0 == 4 * p.w) {
+        upt_ratio<T, VW, 4>(v, s, p.src_ld0, n, y, x, c, p.h, p.w, p.sh0, p.sw0);
+        break;
+      }
       // fine rows/cols whose bilinear stencil can touch coarse (y, x), widened by one
       const float fy = p.align ? (float)(p.sh0 - 1) / (float)max(p.h - 1, 1) : (float)p.sh0 / (float)p.h;
       const float fx = p.align ? (float)(p.sw0 - 1) / (float)max(p.w - 1, 1) : (float)p.sw0 / (float)p.w;
