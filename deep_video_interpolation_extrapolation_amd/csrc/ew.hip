@@ -127,19 +127,37 @@ __device__ __forceinline__ void upt_ratio(float* v, const T* __restrict__ s, lon
     const float wy = upt_weight(Y, y, h, sh, 0);
     if (wy == 0.f) continue;
     const T* srow = s + ((long long)n * sh + Y) * sw * ld + c;
-    float t[NC][VW];
+    if constexpr (VW == 8) {  // bf16: keep the loads packed (4 VGPRs each) until their FMAs
+      i32x4 raw[NC];
 #pragma unroll
-    for (int j = 0; j < NC; ++j) VecN<T, VW>::load(srow + (long long)xo[j] * ld, t[j]);
+      for (int j = 0; j < NC; ++j) raw[j] = *(const i32x4*)(srow + (long long)xo[j] * ld);
 #pragma unroll
-    for (int j = 0; j < NC; ++j)
+      for (int j = 0; j < NC; ++j) {
+        const float wgt = wy * wx[j];
 #pragma unroll
-      for (int k = 0; k < VW; ++k) v[k] += wy * wx[j] * t[j][k];
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += wgt * __uint_as_float(((uint32_t)raw[j][k]) << 16);
+          v[2 * k + 1] += wgt * __uint_as_float(((uint32_t)raw[j][k]) & 0xffff0000u);
+        }
+      }
+    } else {
+      float t[NC][VW];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) VecN<T, VW>::load(srow + (long long)xo[j] * ld, t[j]);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+#pragma unroll
+        for (int k = 0; k < VW; ++k) v[k] += wy * wx[j] * t[j][k];
+    }
   }
 }
 
 // One thread = VW channels of one pixel; blockIdx.y = image row (n, y), so the per-element
 // index math is one 32-bit division by the channel-vector count.
-template <typename T, int VW>
+// OPK >= 0: the kernel is specialised to that op (the others compile away), so the hot
+// multi-resolution ops do not carry the register allocation of the largest case; -1: any op;
+// -2: any op but the upsample adjoint.
+template <typename T, int VW, int OPK>
 __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= p.w * cq) return;
@@ -151,7 +169,7 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
   float v[VW];
 #pragma unroll
   for (int k = 0; k < VW; ++k) v[k] = 0.f;
-  switch (p.op) {
+  switch (OPK >= 0 ? OPK : p.op) {
     case DVIE_EW_FUSE:
       up_sample_add<T, VW>(v, (const T*)p.src0, p.src_ld0, n, y, x, c, p.sh0, p.sw0, p.h, p.w, p.align);
       if (p.nsrc > 1)
@@ -160,6 +178,7 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
         up_sample_add<T, VW>(v, (const T*)p.src2, p.src_ld2, n, y, x, c, p.sh2, p.sw2, p.h, p.w, p.align);
       break;
     case DVIE_EW_UPT: {
+      if constexpr (OPK == -2) break;  // (launched through its own instance)
       // coarse output (y, x) of a (h, w) grid, fine source (sh0, sw0)
       const T* s = (const T*)p.src0;
       if (!p.align && p.sh0 == 2 * p.h && p.sw0 == 2 * p.w) {
@@ -332,12 +351,18 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
   const int cq = d->c / vw;
   const dim3 grid((unsigned)((d->w * cq + 255) / 256), (unsigned)(d->n * d->h));
   if (d->dtype == DVIE_BF16) {
-    if (v8)
-      hipLaunchKernelGGL((ew_kernel<bf16_t, 8>), grid, dim3(256), 0, s, *d, cq);
-    else
-      hipLaunchKernelGGL((ew_kernel<bf16_t, 4>), grid, dim3(256), 0, s, *d, cq);
+    if (v8) {
+      if (d->op == DVIE_EW_FUSE)
+        hipLaunchKernelGGL((ew_kernel<bf16_t, 8, DVIE_EW_FUSE>), grid, dim3(256), 0, s, *d, cq);
+      else if (d->op == DVIE_EW_UPT)
+        hipLaunchKernelGGL((ew_kernel<bf16_t, 8, DVIE_EW_UPT>), grid, dim3(256), 0, s, *d, cq);
+      else
+        hipLaunchKernelGGL((ew_kernel<bf16_t, 8, -2>), grid, dim3(256), 0, s, *d, cq);
+    } else {
+      hipLaunchKernelGGL((ew_kernel<bf16_t, 4, -1>), grid, dim3(256), 0, s, *d, cq);
+    }
   } else {
-    hipLaunchKernelGGL((ew_kernel<float, 4>), grid, dim3(256), 0, s, *d, cq);
+    hipLaunchKernelGGL((ew_kernel<float, 4, -1>), grid, dim3(256), 0, s, *d, cq);
   }
   DVIE_RETURN_LAUNCH();
 }
