@@ -256,7 +256,22 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p)
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   if (q < total4) {
     const float* src = p.ws + (long long)p.co_off * p.ws_k + q * 4;
-    for (int k = sl; k < p.splits; k += SL) {
+    // four slabs' loads issued before their adds: one memory latency per four slabs (a plain
+    // loop waits for each load before issuing the next)
+    int k = sl;
+    for (; k + 3 * SL < p.splits; k += 4 * SL) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const f32x4*)(src + (k + u * SL) * slab);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a0 += v[u][0];
+        a1 += v[u][1];
+        a2 += v[u][2];
+        a3 += v[u][3];
+      }
+    }
+    for (; k < p.splits; k += SL) {
       const f32x4 v = *(const f32x4*)(src + k * slab);
       a0 += v[0];
       a1 += v[1];
