@@ -32,7 +32,7 @@ KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwis
               8: "batchnorm_fwd", 9: "batchnorm_bwd", 10: "head_fwd", 11: "head_bwd"}
 # HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
 # this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
-PMC_DIR = "r02j_pmc"  # tools/pmc_bench.sh on the current tree
+PMC_DIR = "r02m_pmc"  # tools/pmc_bench.sh on the current tree
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", PMC_DIR, "traffic.json")
 
 

@@ -8,7 +8,7 @@ tag=${1:-pmck}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/$tag
 mkdir -p $out
-rx=${PMC_RX:-"conv_halo_kernel|conv_ws_kernel|conv_strip_kernel|conv_nk_kernel|conv1x1_kernel|wgrad_halo_kernel|wgrad_wide_kernel|conv_igemm_kernel|wgrad_kernel"}
+rx=${PMC_RX:-"conv_halo_kernel|conv_ws_kernel|conv_strip_kernel|conv_nk_kernel|conv1x1_kernel|conv1x1_persist_kernel|wgrad_halo_kernel|wgrad_wide_kernel|conv_igemm_kernel|wgrad_kernel"}
 cmd=${PMC_CMD:-"python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --profile-steps 0 --graph 0"}
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
