@@ -9,6 +9,8 @@
 // nets/HRNet.py:219-222,577-580 (+ the sums/LeakyReLU of l.212-225), AvgPool2d of
 // nets/vgg.py:9, preprocess_norm of utils/net_utils.py:11-23, torch.cat of
 // nets/HRNet.py:539,582 (by writing channel slices), and their autograd backward ops.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace dvie {
@@ -324,9 +326,98 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
   VecN<T, VW>::store(yp, v);
 }
 
+// EW_FUSE with two horizontally adjacent output pixels per thread (bf16 x8).  For an
+// upsampled source the pair's bilinear columns are {i0, i1} of the left pixel plus the right
+// pixel's i1 (its i0 is one of the left pixel's: the source step per output pixel is <= 1), so
+// a source costs 2 rows x 3 column loads per pair instead of 2 x 4 per pixel; at 4x the pair
+// shares both columns.  Same lerp arithmetic and summation order as ew_kernel.
+template <typename T, int VW>
+__global__ __launch_bounds__(256) void ew_fuse2_kernel(const dvie_ew_desc p, int cq) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int wp = (p.w + 1) >> 1;
+  if (e >= wp * cq) return;
+  const int xp = e / cq;
+  const int c = (e - xp * cq) * VW;
+  const int x = 2 * xp;
+  const bool two = x + 1 < p.w;
+  const int row = blockIdx.y;
+  const int n = row / p.h, y = row - (row / p.h) * p.h;
+  float v0[VW], v1[VW];
+#pragma unroll
+  for (int k = 0; k < VW; ++k) v0[k] = v1[k] = 0.f;
+  auto src_add = [&](const T* s, long long ld, int sh, int sw) {
+    float a[VW], b[VW];
+    if (sh == p.h && sw == p.w) {
+      VecN<T, VW>::load(s + (((long long)n * sh + y) * sw + x) * ld + c, a);
+      VecN<T, VW>::load(s + (((long long)n * sh + y) * sw + (two ? x + 1 : x)) * ld + c, b);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        v0[k] += a[k];
+        v1[k] += b[k];
+      }
+      return;
+    }
+    const Lerp ly = lerp_src(y, sh, p.h, p.align);
+    const Lerp l0 = lerp_src(x, sw, p.w, p.align), l1 = lerp_src(two ? x + 1 : x, sw, p.w, p.align);
+    const long long r0 = ((long long)n * sh + ly.i0) * sw, r1 = ((long long)n * sh + ly.i1) * sw;
+    // columns: c0 = l0.i0, c1 = l0.i1, c2 = l1.i1; the right pixel's i0 is c0 or c1
+    const bool rsh = l1.i0 != l0.i0;  // right pixel starts at c1
+    float t00[VW], t01[VW], t02[VW], t10[VW], t11[VW], t12[VW];
+    VecN<T, VW>::load(s + (r0 + l0.i0) * ld + c, t00);
+    VecN<T, VW>::load(s + (r0 + l0.i1) * ld + c, t01);
+    VecN<T, VW>::load(s + (r0 + l1.i1) * ld + c, t02);
+    VecN<T, VW>::load(s + (r1 + l0.i0) * ld + c, t10);
+    VecN<T, VW>::load(s + (r1 + l0.i1) * ld + c, t11);
+    VecN<T, VW>::load(s + (r1 + l1.i1) * ld + c, t12);
+#pragma unroll
+    for (int k = 0; k < VW; ++k) {
+      v0[k] += ly.l0 * (l0.l0 * t00[k] + l0.l1 * t01[k]) + ly.l1 * (l0.l0 * t10[k] + l0.l1 * t11[k]);
+      const float ra = rsh ? t01[k] : t00[k], rb = t02[k];
+      const float rc = rsh ? t11[k] : t10[k], rd = t12[k];
+      v1[k] += ly.l0 * (l1.l0 * ra + l1.l1 * rb) + ly.l1 * (l1.l0 * rc + l1.l1 * rd);
+    }
+  };
+  src_add((const T*)p.src0, p.src_ld0, p.sh0, p.sw0);
+  if (p.nsrc > 1) src_add((const T*)p.src1, p.src_ld1, p.sh1, p.sw1);
+  if (p.nsrc > 2) src_add((const T*)p.src2, p.src_ld2, p.sh2, p.sw2);
+  auto finish = [&](int xx, float* v) {
+    const long long pix = (long long)row * p.w + xx;
+    T* yp = (T*)p.y + pix * p.y_ld + c;
+    float t[VW];
+    if (p.res) {
+      VecN<T, VW>::load((const T*)p.res + pix * p.res_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] += t[k];
+    }
+    if (p.beta) {
+      VecN<T, VW>::load(yp, t);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] += t[k];
+    }
+    if (p.act) {
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] = act_fwd(v[k], p.act, p.alpha);
+    }
+    if (p.dact) {
+      VecN<T, VW>::load((const T*)p.z + pix * p.z_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) v[k] *= act_dz(t[k], p.dact, p.alpha);
+    }
+    VecN<T, VW>::store(yp, v);
+  };
+  finish(x, v0);
+  if (two) finish(x + 1, v1);
+}
+
 }  // namespace dvie
 
 using namespace dvie;
+
+// DVIE_EW_FUSE2=0: one output pixel per thread for the fuse op (A/B runs); read per launch
+static bool fuse2_on() {
+  const char* e = getenv("DVIE_EW_FUSE2");
+  return !(e && *e == '0');
+}
 
 extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->c > 0 && d->c % 4 == 0, "ew: c=%d must be a multiple of 4", d ? d->c : -1);
@@ -352,7 +443,13 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
   const dim3 grid((unsigned)((d->w * cq + 255) / 256), (unsigned)(d->n * d->h));
   if (d->dtype == DVIE_BF16) {
     if (v8) {
-      if (d->op == DVIE_EW_FUSE)
+      // (pairs need every source at most the output's size: a source step <= 1 per pixel)
+      const bool up = d->sw0 <= d->w && d->sh0 <= d->h && (d->nsrc < 2 || (d->sw1 <= d->w && d->sh1 <= d->h)) &&
+                      (d->nsrc < 3 || (d->sw2 <= d->w && d->sh2 <= d->h));
+      if (d->op == DVIE_EW_FUSE && up && fuse2_on()) {
+        const dim3 g2((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * d->h));
+        hipLaunchKernelGGL((ew_fuse2_kernel<bf16_t, 8>), g2, dim3(256), 0, s, *d, cq);
+      } else if (d->op == DVIE_EW_FUSE)
         hipLaunchKernelGGL((ew_kernel<bf16_t, 8, DVIE_EW_FUSE>), grid, dim3(256), 0, s, *d, cq);
       else if (d->op == DVIE_EW_UPT)
         hipLaunchKernelGGL((ew_kernel<bf16_t, 8, DVIE_EW_UPT>), grid, dim3(256), 0, s, *d, cq);

@@ -33,7 +33,7 @@ def _desc(op, n, h, w, c, y, y_ld):
 
 
 # (n, fine h, fine w, coarse h, coarse w, c, align)
-CASES = [(2, 64, 128, 16, 32, 64, 0), (2, 64, 128, 32, 64, 32, 0), (1, 77, 130, 10, 17, 16, 0),
+CASES = [(2, 64, 128, 16, 32, 64, 0), (2, 64, 128, 32, 64, 32, 0), (1, 77, 131, 10, 17, 16, 0),
          (2, 64, 128, 16, 32, 64, 1), (1, 40, 72, 20, 36, 24, 1), (1, 96, 64, 12, 8, 8, 0)]
 
 
@@ -57,8 +57,11 @@ def test_upsample_adjoint(dev, case):
     assert err < 1e-2, (case, err)
 
 
+@pytest.mark.parametrize("pairs", ["1", "0"])
 @pytest.mark.parametrize("case", CASES)
-def test_fuse_upsample(dev, case):
+def test_fuse_upsample(dev, case, pairs, monkeypatch):
+    """EW_FUSE with two output pixels per thread (default) and one (DVIE_EW_FUSE2=0)."""
+    monkeypatch.setenv("DVIE_EW_FUSE2", pairs)
     n, H, W, h, w, c, align = case
     g = torch.Generator().manual_seed(5)
     x0 = _bf(torch.randn(n, H, W, c, generator=g))
