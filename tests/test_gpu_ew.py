@@ -84,3 +84,29 @@ def test_fuse_upsample(dev, case, pairs, monkeypatch):
     _run(d)
     err = float((y.float().cpu() - ref).abs().max() / ref.abs().max())
     assert err < 1e-2, (case, err)
+
+
+@pytest.mark.parametrize("norm", [False, True])
+def test_nchw_pack(dev, norm):
+    """EW_NCHW: fp32 NCHW planes (ext_c of c channels, optional (x - mean) / std as
+    preprocess_norm, utils/net_utils.py:11-23) into a bf16 NHWC channel slice; zero channels
+    past ext_c."""
+    n, ec, H, W, c = 2, 6, 37, 301, 24
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, ec, H, W, generator=g)
+    mean = torch.tensor([0.4, 0.5, 0.6, 0.1, 0.2, 0.3] + [0.0] * 2)
+    std = torch.tensor([0.2, 0.3, 0.25, 1.0, 0.5, 2.0] + [1.0] * 2)
+    ref = torch.zeros(n, H, W, c)
+    xr = (x - mean[:ec, None, None]) / std[:ec, None, None] if norm else x
+    ref[..., :ec] = xr.permute(0, 2, 3, 1)
+    buf = torch.full((n, H, W, c + 8), 7.0, dtype=torch.bfloat16, device=dev)
+    xd, md, sd = x.to(dev), mean.to(dev), std.to(dev)
+    d = _desc(L.EW_NCHW, n, H, W, c, buf[..., 8:], c + 8)
+    d.ext, d.ext_c = xd.data_ptr(), ec
+    d.sn, d.sc, d.sh, d.sw = ec * H * W, H * W, W, 1
+    if norm:
+        d.mean, d.std = md.data_ptr(), sd.data_ptr()
+    _run(d)
+    out = buf.float().cpu()
+    assert float((out[..., 8:] - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
+    assert bool((out[..., :8] == 7.0).all()), "write outside the channel slice"
