@@ -110,3 +110,21 @@ def test_nchw_pack(dev, norm):
     out = buf.float().cpu()
     assert float((out[..., 8:] - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
     assert bool((out[..., :8] == 7.0).all()), "write outside the channel slice"
+
+
+@pytest.mark.parametrize("shape", [(70001, 64, 72, 37), (5000, 24, 24, 7), (131072, 448, 448, 64), (999, 8, 16, 3)])
+def test_colsum(dev, shape):
+    """dvie_colsum (bias gradients: per-channel column sums of a bf16 [rows][c] gradient with
+    row pitch ld, split into `splits` row ranges of fp32 partials) vs torch in fp64."""
+    rows, c, ld, splits = shape
+    g = torch.Generator().manual_seed(13)
+    gb = torch.randn(rows, ld, generator=g).to(torch.bfloat16)
+    ref = gb[:, :c].double().sum(0)
+    gd = gb.to(dev)
+    ws = torch.zeros(splits, c, dtype=torch.float32, device=dev)
+    d = L.ColsumDesc()
+    d.g, d.ws, d.g_ld, d.rows, d.c, d.splits, d.dtype = gd.data_ptr(), ws.data_ptr(), ld, rows, c, splits, L.BF16
+    L.check(L.load().dvie_colsum(ctypes.byref(d), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "colsum")
+    torch.cuda.synchronize()
+    out = ws.double().sum(0).cpu()
+    assert float((out - ref).abs().max()) <= 1e-4 * float(ref.abs().max()) + 1e-3
