@@ -46,13 +46,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (clips)")
-    ap.add_argument("--height", type=int, default=256)
-    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (clips); default: the workload's")
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
     ap.add_argument("--ops-out", default=None, help="write the per-op profile table (profiling steps) here")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
+                    help="c2: BASELINE configs[1] (InterNet 256x512 bf16, batch 8; the default line); c5: "
+                         "BASELINE configs[4] per GPU (two-stage extrapolation ExtraStage3Net 1024x2048 bf16, batch "
+                         "1, hipGraph-captured step)")
     ap.add_argument("--graph", type=int, default=1, help="1: time the hipGraph-captured step (runners/graph.py), "
                                                            "0: the eager step")
     return ap.parse_args()
@@ -100,6 +104,26 @@ def cpu_baseline(H, W, steps=2):
             "c1_frames_per_s": round(8 / dt1, 4),
             "sample": f"{steps} InterTrainer steps of the CPU oracle (fp32) at {H}x{W}, batch {B} ({dt:.1f}s), after "
                       f"one untimed warm-up step; C1: 8 triplets at 128x256 in 4 steps of batch 2 ({dt1:.1f}s)"}
+
+
+def cpu_baseline_c5(H=256, W=512):
+    """CPU oracle two-stage extrapolation step (oracle.step.extra_refine_step, fp32) on a
+    bounded sample: one step of batch 1 at H x W (a 1024x2048 step takes minutes on the
+    host), after an untimed warm-up step at 64x128; `value` is that sample's frames/s and
+    `per_pixel_scaled` the same rate scaled to 1024x2048 frames by pixel count."""
+    from oracle import hrnet, losses, refine, step
+    threads = torch.get_num_threads()
+    Pc, vs = hrnet.init_params(1024), losses.synthetic_vgg19_state()
+    Pr, Ps = refine.init_params(None, refine.srn_specs()), refine.init_params(None, refine.attn_specs())
+    step.extra_refine_step(Pc, Pr, vs, step.synthetic_batch(1, 64, 128), 3, Ps=Ps, prop=True)
+    t = time.time()
+    step.extra_refine_step(Pc, Pr, vs, step.synthetic_batch(1, H, W), 3, Ps=Ps, prop=True)
+    dt = time.time() - t
+    return {"value": round(1 / dt, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "per_pixel_scaled": round(1 / dt * (H * W) / (1024 * 2048), 5), "os_cpu_count": os.cpu_count(),
+            "cpu_model": _cpu_model(),
+            "sample": f"1 two-stage extrapolation step of the CPU oracle (fp32, n_sc 3, stage3_prop) at {H}x{W}, "
+                      f"batch 1 ({dt:.1f}s), after one untimed warm-up step at 64x128"}
 
 
 def warp_roofline(dev, n, H, W, reps=20):
@@ -178,9 +202,9 @@ def clip_prep_roofline(dev, n, H, W, reps=20):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    gbs = 100.0 * n * 3 * H * W / (ms * 1e-3) / 1e9
+    gbs = 96.0 * n * 3 * H * W / (ms * 1e-3) / 1e9
     return {"clips": n, "frames": 3 * n, "shape": [H, W], "ms": round(ms, 4), "GBps": round(gbs, 1),
-            "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_px": 100,
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_px": 96,
             "note": "per batch call incl. its small host->device index/param copies and output allocation"}
 
 
@@ -201,8 +225,15 @@ def _free_port():
     return p
 
 
+# per-GPU batch and frame size of each workload (BASELINE.json configs[1] / configs[4])
+WORKLOAD_SHAPE = {"c2": dict(batch=8, height=256, width=512), "c5": dict(batch=1, height=1024, width=2048)}
+
+
 def main():
     a = parse()
+    for k, v in WORKLOAD_SHAPE[a.workload].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # nothing has touched the GPU yet: run the N ranks as a child torchrun and exit with
         # its status (never exec from here)
@@ -225,12 +256,23 @@ def main():
     from deep_video_interpolation_extrapolation_amd.options import default_args
     from deep_video_interpolation_extrapolation_amd.runners.InterTrainer import InterTrainer
 
-    args = default_args("INTER", syn_type="inter", mode="xs2xs", interval=5, vid_length=1, train_coarse=True,
-                        batch_size=a.batch * world, input_h=a.height, input_w=a.width, precision=a.precision,
-                        synthetic=a.batch * world, num_workers=0, split="train", rank=rank, gpus=world)
+    common = dict(mode="xs2xs", vid_length=1, train_coarse=True, batch_size=a.batch * world, input_h=a.height,
+                  input_w=a.width, precision=a.precision, synthetic=a.batch * world, num_workers=0, split="train",
+                  rank=rank, gpus=world)
+    if a.workload == "c5":
+        from deep_video_interpolation_extrapolation_amd.runners.ExtraTrainer import ExtraTrainer
+        # the reference's own two-stage command line (cmd:158): --n_sc 3 --stage3 --stage3_prop,
+        # here with all three nets trained
+        args = default_args("EXTRA", syn_type="extra", interval=9, model="ExtraStage3Net", refine=True,
+                            refine_model="SRNRefine", stage3=True, stage3_prop=True, n_scales=3, train_refine=True,
+                            train_stage3=True, **common)
+        trainer_cls = ExtraTrainer
+    else:
+        args = default_args("INTER", syn_type="inter", interval=5, **common)
+        trainer_cls = InterTrainer
     args.logger = _StderrLog()  # stdout carries the one JSON line only
     torch.manual_seed(args.seed)
-    trainer = InterTrainer(args)
+    trainer = trainer_cls(args)
     data = make_batch(a.batch, a.height, a.width, dev, rank * a.batch)
 
     def timed(fn):
@@ -260,7 +302,10 @@ def main():
         from deep_video_interpolation_extrapolation_amd.runners.graph import GraphedStep
         gstep = GraphedStep(trainer, data, warmup=1)  # the batch now lives in the graph's static inputs
         dt, ld = timed(lambda _d: gstep.step())
-    loss_all = float(ld["loss_all"])
+        loss_all = float(ld["loss_all"])
+        gstep.close()  # eager profiling steps below: in-backward bucket overlap back on (W > 1)
+    else:
+        loss_all = float(ld["loss_all"])
 
     # ---- profiling steps: per-op HIP events on the launch stream ----
     prof = []
@@ -332,8 +377,10 @@ def main():
 
     if rank == 0:
         frames = a.batch * world * a.steps
+        c5 = a.workload == "c5"
         out = {
-            "metric": "train frames/s (256x512 len-3 clips)",
+            "metric": ("train frames/s (1024x2048 len-3 clips, two-stage extrapolation)" if c5
+                       else "train frames/s (256x512 len-3 clips)"),
             "value": round(frames / dt, 3),
             "unit": "frames/s",
             "n_gpus": world,
@@ -345,7 +392,9 @@ def main():
             "vs_baseline": None,
             "dtype": a.precision,
             "data": "synthetic (seeded Cityscapes-shaped triplets, HBM-resident); random-init HRNet, synthetic VGG19",
-            "config": {"workload": f"InterNet int_5_len_3 train step {a.height}x{a.width} {a.precision}",
+            "config": {"workload": (f"ExtraStage3Net (HRNet + SRNRefine + MSResAttnRefine, n_sc 3, stage3_prop) "
+                                    f"int_9_len_3 train step {a.height}x{a.width} {a.precision}" if c5 else
+                                    f"InterNet int_5_len_3 train step {a.height}x{a.width} {a.precision}"),
                        "per_gpu_batch": a.batch, "global_batch": a.batch * world, "parallelism": f"dp{world}",
                        "step": "hipGraph-captured" if a.graph else "eager"},
             "eager_ms_per_step": round(eager_dt * 1e3 / a.steps, 3),
@@ -353,11 +402,18 @@ def main():
             "loss_all": loss_all,
             "step_breakdown_ms": {k: round(v["ms"] / max(1, a.profile_steps), 3) for k, v in sorted(agg.items())},
         }
-        out["warp"] = warp_roofline(dev, a.batch, a.height, a.width)
-        out["warp_1024x2048"] = warp_roofline(dev, a.batch, 1024, 2048, reps=5)  # BASELINE configs[4] frames
-        out["clip_prep"] = clip_prep_roofline(dev, a.batch, a.height, a.width)
+        at = [agg[c] for c in ("attn", "attn_bwd") if c in agg]
+        if at:  # local-window attention of the stage-3 net (HBM-bound gathers / reductions)
+            ms, by = sum(r["ms"] for r in at), sum(r["bytes"] for r in at)
+            out["attn"] = {"ms_per_step": round(ms / a.profile_steps, 3), "launches_per_step": sum(r["n"] for r in at)
+                           // a.profile_steps, "GBps": round(by / (ms * 1e-3) / 1e9, 1),
+                           "frac": round(by / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+        if not c5:
+            out["warp"] = warp_roofline(dev, a.batch, a.height, a.width)
+            out["warp_1024x2048"] = warp_roofline(dev, a.batch, 1024, 2048, reps=5)  # BASELINE configs[4] frames
+            out["clip_prep"] = clip_prep_roofline(dev, a.batch, a.height, a.width)
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(a.height, a.width)
+            out["cpu_baseline"] = cpu_baseline_c5() if c5 else cpu_baseline(a.height, a.width)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -881,10 +881,22 @@ class Plan:
         K = op.wh * op.ww
         ld_a = a.buf.C
 
+        npx = nb * out.H * out.W
+        J = op.nhalf * K
+        cb = sum(b.c for b in op.bs)
+        # algorithmic channels touched per pixel by each backward kernel (profiling meta):
+        # its reads (upstream gradient, saved operands) and its written gradient
+        moved = {"l2norm": 4 * op.c, "softmax": 3 * J, "wnorm": 4 * J, "pool": 2 * op.c,
+                 "corr": op.c + J + cb, "gather": out.c + J + cb}[op.kind]
+
         def contrib(region, build):
             if region.buf.needs_grad:
-                self._contrib(region, lambda beta, res, res_ld, dact, z, z_ld:
-                              [build(dict(res=res, res_ld=res_ld, dact=dact, z=z, z_ld=z_ld, beta=beta))])
+                def emit(beta, res, res_ld, dact, z, z_ld):
+                    o = build(dict(res=res, res_ld=res_ld, dact=dact, z=z, z_ld=z_ld, beta=beta))
+                    o.meta = dict(cls="attn_bwd", name=f"{op.kind}:{region.buf.name}", flops=0.0,
+                                  bytes=float(self.es * npx * moved))
+                    return [o]
+                self._contrib(region, emit)
 
         if op.kind == "l2norm":  # a = x, out = x / |x|
             contrib(a, lambda e: self.attn_desc(L.ATTN_L2NORM_BWD, nb, hw, op.c, gout, gld, self.ptr(a, grad=True),

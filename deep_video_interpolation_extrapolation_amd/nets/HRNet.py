@@ -439,6 +439,7 @@ class HRNet(FlatParams, nn.Module):
 
     # DVIE_FUSE_HEADS=0: the two 1x1 head convs as separate launches (A/B runs)
     fuse_heads = os.environ.get("DVIE_FUSE_HEADS", "1") != "0"
+    _stack_limit = 0xFFFFFF00  # bytes of one image of the stacked hidden map (32-bit buffer range)
 
     def _heads(self, g, cat):
         """rgb_layer / seg_layer (nets/HRNet.py:410-442 of the reference).  Both start with a
@@ -454,7 +455,7 @@ class HRNet(FlatParams, nn.Module):
         # buffer range: keep the two hidden maps separate where 2x448 channels exceed it
         # (fp32 at 1024x2048)
         es = 2 if g.dtype == torch.bfloat16 else 4
-        fits = H * W * 2 * last * es < 0xFFFFFF00
+        fits = H * W * 2 * last * es < self._stack_limit
         if st and fits and (getattr(g, "dry", False) or st.contiguous()):
             hh = g.buffer("heads_hidden", H, W, 2 * last)
             g.conv(cat, st, E.R(hh), act=A.ACT_LRELU, name="heads.0")
@@ -533,11 +534,15 @@ class HRNet(FlatParams, nn.Module):
                 ps = [lay.m.weight] + ([lay.m.bias] if lay.m.bias is not None else [])
             hi = max([hi] + [end[id(p)] for p in ps])
             done += sum(p.numel() for p in ps)
-            assert done == hi, "parameter gradients must complete in flat-buffer order"
-            if (hi - last) * 4 >= bucket_bytes and hi < total:
+            # the flat layout comes from a dry lowering where the two 448-channel head convs
+            # are one stacked layer ([rgb.w, seg.w, rgb.b, seg.b]); a plan that keeps them
+            # separate (fp32 at 1024x2048, `fits` in _heads) completes them one by one, so a
+            # prefix [0, hi) is final only once every parameter below hi has completed
+            if done == hi and (hi - last) * 4 >= bucket_bytes and hi < total:
                 cuts.append(idx)
                 ranges.append((last, hi))
                 last = hi
+        assert done == total, "every parameter gradient must complete in the backward plan"
         ranges.append((last, total))
         plan.__dict__[key] = (cuts, ranges)
         return cuts, ranges

@@ -12,3 +12,4 @@ from .InterGANNet import InterGANNet, channel_softmax
 from .UNet import SegEncoder, SepUNet, UNet, double_conv, down, inconv, outconv, up
 from .refine import MSResAttnRefine, SRNRefine
 from .InterRefineNet import InterRefineNet, InterStage3Net
+from .ExtraNet import ExtraRefineNet, ExtraStage3Net

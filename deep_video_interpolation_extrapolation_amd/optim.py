@@ -29,6 +29,7 @@ class _FusedOptimizer(torch.optim.Optimizer):
         self._flat = {}
         self.capturable = False
         self._dsteps = {}
+        self._split = {}  # capturable: group index -> per-parameter step counts differ
 
     def _launch(self, p, g, s0, s1, n, group, step, device):
         raise NotImplementedError
@@ -46,6 +47,7 @@ class _FusedOptimizer(torch.optim.Optimizer):
                 if "step" in st and torch.is_tensor(st["step"]) and st["step"].is_cuda:
                     st["step"] = st["step"].detach().cpu().clone()
             self._dsteps = {}
+        self._split = {}
 
     def _dev_step(self, key, params, device):
         """one device step tensor shared by `params` (created from their host count)"""
@@ -57,6 +59,22 @@ class _FusedOptimizer(torch.optim.Optimizer):
         for p in params:
             self.state[p]["step"] = d
         return d
+
+    def _counts_differ(self, gi, ps):
+        """Whether the group's parameters carry different step counts.  Eager: checked on
+        the host counts every step.  Capturable: decided once, on the host counts of the
+        first (eager) step after set_capturable, and kept -- counts that differ once keep
+        differing by the same lag, and a captured step must not read device counts back."""
+        if self.capturable and gi in self._split:
+            return self._split[gi]
+        counts = set()
+        for p in ps:
+            st = self.state[p].get("step", 0.0)
+            counts.add(float(st.cpu()) if torch.is_tensor(st) else float(st))
+        differ = len(counts) > 1
+        if self.capturable:
+            self._split[gi] = differ
+        return differ
 
     def _flat_group(self, gi, group):
         """(owner, flat state 0, flat state 1) if the group maps onto one flat buffer."""
@@ -74,8 +92,7 @@ class _FusedOptimizer(torch.optim.Optimizer):
             g = p.grad
             if g is None or g.data_ptr() != fg.data_ptr() + (p.data_ptr() - flat.data_ptr()):
                 return None
-        if not self.capturable and len({float(self.state[p]["step"]) if "step" in self.state[p] else 0.0
-                                        for p in ps}) > 1:
+        if self._counts_differ(gi, ps):
             return None  # per-parameter step counts differ (SN u, v become trainable after step 1)
         k0, k1 = self.STATE
         ent = self._flat.get(gi)
@@ -145,6 +162,7 @@ class _FusedOptimizer(torch.optim.Optimizer):
         super().load_state_dict(state_dict)
         self._flat = {}  # re-bind flat state views (copies loaded values in _flat_group)
         self._dsteps = {}
+        self._split = {}
 
 
 class Adamax(_FusedOptimizer):

@@ -63,50 +63,11 @@ GLOBAL = [
     ("--clip_store", "clip_store", str, None, None),
 ]
 
-EXTRA = [
-    ("--model", "model", str, "ExtraNet", ["ExtraNet", "ExtraInpaintNet"]),
-    ("--load_model", "load_model", str, "ExtraNet", ["ExtraNet", "ExtraInpaintNet"]),
-    ("--coarse_model", "coarse_model", str, "HRNet", ["HRNet"]),
-    ("--coarse_o", "coarse_optimizer", str, "adamax", _ADAMAX),
-    ("--coarse_lr", "coarse_learning_rate", float, 0.001, None),
-    ("--load_coarse", "load_coarse", bool, False, None),
-    ("--train_coarse", "train_coarse", bool, False, None),
-    ("--inpaint", "inpaint", bool, False, None),
-    ("--inpaint_mask", "inpaint_mask", bool, False, None),
-    ("--inpaint_model", "inpaint_model", str, "InpaintUnet", ["InpaintUnet"]),
-    ("--inpaint_o", "inpaint_optimizer", str, "adamax", _ADAMAX),
-    ("--inpaint_lr", "inpaint_learning_rate", float, 0.001, None),
-    ("--load_inpaint", "load_inpaint", bool, False, None),
-    ("--train_inpaint", "train_inpaint", bool, False, None),
-    ("--num_pred_once", "num_pred_once", int, 1, None),
-    ("--num_pred_step", "num_pred_step", int, 1, None),
-    ("--fix_init_frames", "fix_init_frames", bool, False, None),
-]
-
-_DISC_FRAME = ["FrameDiscriminator", "FrameLocalDiscriminator", "FrameSNDiscriminator", "FrameSNLocalDiscriminator",
-               "FrameDetDiscriminator", "FrameSNDetDiscriminator", "FrameLSSNDetDiscriminator"]
-_DISC_VIDEO = ["VideoDiscriminator", "VideoLocalDiscriminator", "VideoSNDiscriminator", "VideoSNLocalDiscriminator",
-               "VideoDetDiscriminator", "VideoSNDetDiscriminator", "VideoLSSNDetDiscriminator",
-               "VideoLocalPatchSNDetDiscriminator", "VideoVecSNDetDiscriminator", "VideoPoolSNDetDiscriminator",
-               "VideoGlobalZeroSNDetDiscriminator", "VideoGlobalResSNDetDiscriminator",
-               "VideoGlobalMaskSNDetDiscriminator", "VideoGlobalCoordSNDetDiscriminator"]
-_INTER_MODELS = ["InterNet", "InterRefineNet", "InterStage3Net", "InterGANNet"]
-
-INTER = [
-    ("--model", "model", str, "InterNet", _INTER_MODELS),
-    ("--load_model", "load_model", str, "InterNet", _INTER_MODELS),
+# second-stage flags of the reference's INTER sub-command (options/options.py:296-380);
+# the EXTRA sub-command takes them too for the build-defined extrapolation two-stage nets
+# (nets/ExtraNet.py ExtraRefineNet / ExtraStage3Net, BASELINE config 5)
+REFINE = [
     ("--n_sc", "n_scales", int, 1, None),
-    ("--gan", "gan", bool, False, None),
-    ("--coarse_model", "coarse_model", str, "HRNet", ["HRNet", "VAEHRNet"]),
-    ("--coarse_o", "coarse_optimizer", str, "adamax", _ADAMAX),
-    ("--coarse_lr", "coarse_learning_rate", float, 0.001, None),
-    ("--load_coarse", "load_coarse", bool, False, None),
-    ("--train_coarse", "train_coarse", bool, False, None),
-    ("--vae", "vae", bool, False, None),
-    ("--seg_disc", "seg_disc", bool, False, None),
-    ("--track_gen", "track_gen", bool, False, None),
-    ("--track_gen_model", "track_gen_model", str, "TrackGen", ["TrackGen", "TrackGenV2"]),
-    ("--loc_diff_w", "loc_diff_weight", float, 100, None),
     ("--refine", "refine", bool, False, None),
     ("--with_gt_seg", "with_gt_seg", bool, False, None),
     ("--refine_model", "refine_model", str, "refineUnet", ["refineUnet", "SRNRefine"]),
@@ -125,6 +86,53 @@ INTER = [
      ["MSResAttnRefine", "MSResAttnRefineV2", "MSResAttnRefineV2Base", "MSResAttnRefineV3"]),
     ("--stage3_prop", "stage3_prop", bool, False, None),
     ("--stage3_flow_consist_w", "stage3_flow_consist_weight", float, 0, None),
+]
+
+_EXTRA_MODELS = ["ExtraNet", "ExtraInpaintNet", "ExtraRefineNet", "ExtraStage3Net"]
+EXTRA = [
+    ("--model", "model", str, "ExtraNet", _EXTRA_MODELS),
+    ("--load_model", "load_model", str, "ExtraNet", _EXTRA_MODELS),
+    ("--coarse_model", "coarse_model", str, "HRNet", ["HRNet"]),
+    ("--coarse_o", "coarse_optimizer", str, "adamax", _ADAMAX),
+    ("--coarse_lr", "coarse_learning_rate", float, 0.001, None),
+    ("--load_coarse", "load_coarse", bool, False, None),
+    ("--train_coarse", "train_coarse", bool, False, None),
+    ("--inpaint", "inpaint", bool, False, None),
+    ("--inpaint_mask", "inpaint_mask", bool, False, None),
+    ("--inpaint_model", "inpaint_model", str, "InpaintUnet", ["InpaintUnet"]),
+    ("--inpaint_o", "inpaint_optimizer", str, "adamax", _ADAMAX),
+    ("--inpaint_lr", "inpaint_learning_rate", float, 0.001, None),
+    ("--load_inpaint", "load_inpaint", bool, False, None),
+    ("--train_inpaint", "train_inpaint", bool, False, None),
+    ("--num_pred_once", "num_pred_once", int, 1, None),
+    ("--num_pred_step", "num_pred_step", int, 1, None),
+    ("--fix_init_frames", "fix_init_frames", bool, False, None),
+] + REFINE
+
+_DISC_FRAME = ["FrameDiscriminator", "FrameLocalDiscriminator", "FrameSNDiscriminator", "FrameSNLocalDiscriminator",
+               "FrameDetDiscriminator", "FrameSNDetDiscriminator", "FrameLSSNDetDiscriminator"]
+_DISC_VIDEO = ["VideoDiscriminator", "VideoLocalDiscriminator", "VideoSNDiscriminator", "VideoSNLocalDiscriminator",
+               "VideoDetDiscriminator", "VideoSNDetDiscriminator", "VideoLSSNDetDiscriminator",
+               "VideoLocalPatchSNDetDiscriminator", "VideoVecSNDetDiscriminator", "VideoPoolSNDetDiscriminator",
+               "VideoGlobalZeroSNDetDiscriminator", "VideoGlobalResSNDetDiscriminator",
+               "VideoGlobalMaskSNDetDiscriminator", "VideoGlobalCoordSNDetDiscriminator"]
+_INTER_MODELS = ["InterNet", "InterRefineNet", "InterStage3Net", "InterGANNet"]
+
+INTER = [
+    ("--model", "model", str, "InterNet", _INTER_MODELS),
+    ("--load_model", "load_model", str, "InterNet", _INTER_MODELS),
+    ("--gan", "gan", bool, False, None),
+    ("--coarse_model", "coarse_model", str, "HRNet", ["HRNet", "VAEHRNet"]),
+    ("--coarse_o", "coarse_optimizer", str, "adamax", _ADAMAX),
+    ("--coarse_lr", "coarse_learning_rate", float, 0.001, None),
+    ("--load_coarse", "load_coarse", bool, False, None),
+    ("--train_coarse", "train_coarse", bool, False, None),
+    ("--vae", "vae", bool, False, None),
+    ("--seg_disc", "seg_disc", bool, False, None),
+    ("--track_gen", "track_gen", bool, False, None),
+    ("--track_gen_model", "track_gen_model", str, "TrackGen", ["TrackGen", "TrackGenV2"]),
+    ("--loc_diff_w", "loc_diff_weight", float, 100, None),
+] + REFINE + [
     ("--local_disc", "local_disc", bool, False, None),
 ]
 for _kind, _choices in (("frame_disc", _DISC_FRAME), ("frame_det_disc", _DISC_FRAME),

@@ -17,6 +17,9 @@ Reference defects this build does not reproduce:
     onehot(argmax(coarse_seg))], gradients flowing back through coarse_img into the
     previous step (as the reference graph would, had it run).
   * l.188 `d[...]:0` (annotation, not assignment) only affects rank-0 logging.
+With `--refine [--stage3]` (model ExtraRefineNet / ExtraStage3Net, build-defined two-stage
+extrapolation nets for BASELINE config 5) the step adds the second-stage losses per scale
+as the reference InterTrainer does (l.415-425).
 The inpainting branch (`--inpaint`, InpaintUnet) has no model definition anywhere in the
 reference tree and raises NotImplementedError here.
 """
@@ -59,6 +62,7 @@ class ExtraTrainer(InterTrainer):
         npo, nps = getattr(a, "num_pred_once", 1), getattr(a, "num_pred_step", 1)
         if nps > 1:
             assert npo == 1, "rollout (num_pred_step > 1) requires num_pred_once == 1 (reference l.252-253)"
+        assert not self.refine or nps == 1, "the two-stage nets train one-step predictions (num_pred_step 1)"
         data = batch_to(data, self.device)
         # a rollout runs HRNet's backward nps times into one flat gradient: reduce it once,
         # after the last backward (see GradSync.set_overlap)
@@ -85,6 +89,8 @@ class ExtraTrainer(InterTrainer):
                 if xs2xs:
                     loss_dict[prefix + "_ce_loss"] = a.ce_weight * self.SegLoss(
                         coarse_seg[:, 20 * j:20 * j + 20], gt_seg[:, 20 * j:20 * j + 20])
+            if self.refine:
+                self._refine_losses(loss_dict, out, gt_x, "step_{}_frame_1_".format(ii + 1))
             if nps == 1:
                 break
             last_rgb = torch.cat([x[:, -3:], coarse_img], dim=1)
@@ -94,9 +100,23 @@ class ExtraTrainer(InterTrainer):
         for v in loss_dict.values():
             loss = loss + torch.mean(v)
         loss_dict["loss_all"] = loss
-        self.coarse_opt.zero_grad(set_to_none=True)
+        for o in self._opts():
+            o.zero_grad(set_to_none=True)
         (loss / self.W).backward()  # reference `sync` divides loss_all by W in place (l.317, 760-765)
         return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
+
+    def _refine_losses(self, loss_dict, out, gt_x, prefix):
+        """Second-stage losses of the two-stage extrapolation nets (ExtraRefineNet /
+        ExtraStage3Net), the structure of the reference InterTrainer's (l.415-425): per scale
+        the refine RGBLoss and (--stage3) the stage-3 RGBLoss against the target frame
+        resized to that scale; keys '<prefix>refine_<scale>_*' / '<prefix>stage3_<scale>_*'."""
+        a = self.args
+        for i in range(a.n_scales):
+            tag = str(1 / (2 ** (a.n_scales - i - 1)))
+            gts = self._scale_gt(gt_x, i)
+            loss_dict.update(self.refine_RGBLoss(out[2][i], gts, False, prefix=prefix + "refine_" + tag))
+            if self.stage3:
+                loss_dict.update(self.refine_RGBLoss(out[3][i], gts, False, prefix=prefix + "stage3_" + tag))
 
     def validate(self):
         """Reference l.421-583: per (step, frame) L1 / PSNR / SSIM / IoU / VGG-cos."""

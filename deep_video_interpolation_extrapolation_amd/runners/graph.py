@@ -60,6 +60,25 @@ class GraphedStep:
             self.graphs = (self.graph, self.graph2)
         trainer.global_step = g0  # capture ran no step
 
+    def close(self):
+        """Give the trainer back its eager form: optimizers leave capturable mode (step counts
+        return to the host, as checkpoints store them) and, at W > 1, the in-backward bucket
+        all-reduces are on again.  The captured graphs are released."""
+        tr = self.tr
+        for o in tr._opts():
+            o.set_capturable(False)
+        if self.split:
+            tr.no_overlap = False
+            tr.model.set_overlap(True)
+        self.graph = self.graph2 = None
+        self.graphs = ()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     def __call__(self, data=None):
         return self.step(data)
 

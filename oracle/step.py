@@ -183,3 +183,16 @@ def refine_step(Pc, Pr, vgg_state, data, n_scales, Ps=None, prop=False, lr=1e-3,
     grads = {k: {n: v.grad.detach().clone() for n, v in d.items()} for k, d in P.items()}
     new = {k: adamax(parts[k], grads[k], lr)[0] for k in parts}
     return OrderedDict((k, float(v.detach())) for k, v in ld.items()), grads, new
+
+
+def extra_refine_step(Pc, Pr, vgg_state, data, n_scales, Ps=None, prop=False, lr=1e-3):
+    """One ExtraTrainer step with --refine [--stage3] on the build-defined extrapolation
+    two-stage nets (frames 1, 2 -> frame 3; deep_video_interpolation_extrapolation_amd/
+    nets/ExtraNet.py).  With one predicted frame the extrapolation HRNet has the
+    interpolation HRNet's shapes, so this is refine_step on the remapped sample (as
+    extra_step is inter_step), keys prefixed 'step_1_frame_1_'."""
+    remap = {"frame1": data["frame1"], "frame3": data["frame2"], "frame2": data["frame3"],
+             "seg1": data["seg1"], "seg3": data["seg2"], "seg2": data["seg3"]}
+    ld, grads, new = refine_step(Pc, Pr, vgg_state, remap, n_scales, Ps=Ps, prop=prop, lr=lr)
+    ren = OrderedDict((k if k == "loss_all" else "step_1_frame_1_" + k, v) for k, v in ld.items())
+    return ren, grads, new
