@@ -142,11 +142,20 @@ class PlanFunction(torch.autograd.Function):
     `forward(plan_inputs) -> (plan, outputs)` and `backward(plan, grads) -> input grads`.
     """
 
+    @classmethod
+    def apply(cls, runner, n_in, *args):
+        # ctx.needs_input_grad reports requires_grad even under torch.no_grad(), and grad
+        # mode is always off inside forward: record the caller's mode, so an inference
+        # forward compiles (and allocates) no backward
+        runner._grad_mode = torch.is_grad_enabled()
+        return super().apply(runner, n_in, *args)
+
     @staticmethod
     def forward(ctx, runner, n_in, *args):
         inputs = args[:n_in]
         runner._in_needs = tuple(ctx.needs_input_grad[2:2 + n_in])  # which inputs want a gradient
-        plan, outs = runner.run_forward(inputs, any(ctx.needs_input_grad))
+        train = getattr(runner, "_grad_mode", True) and any(ctx.needs_input_grad)
+        plan, outs = runner.run_forward(inputs, train)
         ctx.runner = runner
         ctx.token = _Token(plan) if plan is not None and plan.backward_enabled else None
         ctx.n_in = n_in

@@ -12,6 +12,7 @@ ExtraTrainer --refine --stage3, as a hipGraph-captured step at 1024x2048.
 * bf16 output quality of the two-stage forward at 1024x2048 against the fp32 path
   (coarse, last refine and last stage-3 image): PSNR and relative L2 gated.
 """
+import gc
 import math
 
 import numpy as np
@@ -89,6 +90,7 @@ def test_c5_graphed_two_stage_step_replays_eager(dev):
     eager = [{k: float(v) for k, v in a.step(data).items()} for _ in range(N)]
     flats_a = [m._flat.detach().float().cpu() for m in a.model.flat_owners]
     del a
+    gc.collect()
     torch.cuda.empty_cache()
     b = _trainer(**C5)
     gs = GraphedStep(b, data, warmup=2)
@@ -107,6 +109,9 @@ def test_c5_graphed_two_stage_step_replays_eager(dev):
         fb = m._flat.detach().float().cpu()
         assert float((fa - fb).abs().max()) <= 1e-5 * max(1.0, float(fa.abs().max())), float((fa - fb).abs().max())
     gs.close()
+    del gs, b
+    gc.collect()
+    torch.cuda.empty_cache()
 
 
 def _psnr_pm1(a, b):
@@ -121,6 +126,8 @@ def test_c5_two_stage_bf16_quality_vs_fp32(dev):
     test_gpu_refine): PSNR >= 40 dB on the coarse, last refine and last stage-3 images
     (mapped from [-1, 1] to [0, 1]) and relative L2 < 5e-2."""
     from deep_video_interpolation_extrapolation_amd import nets
+    gc.collect()
+    torch.cuda.empty_cache()
     x, seg = inputs.hrnet_input(1, 1024, 2048)
     outs = {}
     for prec in ("fp32", "bf16"):
@@ -130,6 +137,7 @@ def test_c5_two_stage_bf16_quality_vs_fp32(dev):
             c_rgb, _, ref, re, _ = m(x.to(dev), seg=seg.to(dev))
         outs[prec] = [t.detach().float().cpu() for t in (c_rgb, ref[-1], re[-1])]
         del m, c_rgb, ref, re
+        gc.collect()
         torch.cuda.empty_cache()
     res = [(_psnr_pm1(b, f), rel_l2(b, f)) for b, f in zip(outs["bf16"], outs["fp32"])]
     print("C5 bf16 vs fp32 (coarse, refine, stage3): PSNR dB / relative L2 " +
