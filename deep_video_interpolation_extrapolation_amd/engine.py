@@ -1494,11 +1494,13 @@ class Plan:
 
     def activation_signs(self):
         """{buffer name: bool NCHW CPU tensor (value > 0)} for every buffer written by a
-        LeakyReLU-activated op in the last forward (test support: which branch each
-        activation took, so an fp64 oracle can be evaluated on the same branches)."""
+        LeakyReLU- or ReLU-activated op in the last forward (test support: which branch each
+        activation took, so an fp64 oracle can be evaluated on the same branches).  A buffer
+        with other producers too (the HRNet concat) is included whole; the caller reads the
+        channel slice its activated producer wrote."""
         out = {}
         for b in self.g.buffers:
-            if b.t is not None and b.producers and all(p.act == L.ACT_LRELU for p in b.producers):
+            if b.t is not None and any(p.act in (L.ACT_LRELU, L.ACT_RELU) for p in b.producers):
                 out[b.name] = (b.t > 0).permute(0, 3, 1, 2).cpu()
         return out
 

@@ -512,6 +512,7 @@ class HRNet(FlatParams, nn.Module):
         plan.set_output("rgb", rgb)
         plan.set_output("segout", segout)
         plan.run_forward()
+        self.last_plan = plan
         return plan, (rgb.permute(0, 3, 1, 2)[:, :self.rgb_out_dim], segout.permute(0, 3, 1, 2)[:, :self.seg_out_dim])
 
     # set by runners.comm.GradSync: (bucket_bytes, fn(lo, hi)) called as soon as the flat

@@ -130,6 +130,7 @@ class my_vgg(nn.Module):
         plan.set_input("pred", pred)
         plan.set_input("gt", gt)
         plan.run_forward()
+        self.last_plan = plan
         return plan, (plan.l1_out[:len(FEATURE_TAPS)].sum() / len(FEATURE_TAPS),)
 
     def run_backward(self, plan, inputs, grads, needs):

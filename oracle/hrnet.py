@@ -87,14 +87,28 @@ def _conv(P, name, x, s=1, p=None):
     return F.conv2d(x, w, P.get(name + ".bias"), stride=s, padding=k // 2 if p is None else p)
 
 
-def _lrelu(x):
-    return F.leaky_relu(x, 0.2)
+def _lrelu(x, masks=None, name=None):
+    """LeakyReLU(0.2); with `masks` (plan activation-buffer name -> bool NCHW tensor of the
+    branch the implementation under test took, Plan.activation_signs) the branch decisions
+    are imposed, so that an fp64 oracle can check an fp32 implementation's gradients without
+    LeakyReLU kink flips (an activation within rounding of zero taking the other branch)
+    dominating the comparison.  `name` may carry a channel slice: (buffer, c0, c)."""
+    if masks is None or name is None:
+        return F.leaky_relu(x, 0.2)
+    key, c0, c = name if isinstance(name, tuple) else (name, 0, None)
+    if key not in masks:
+        return F.leaky_relu(x, 0.2)
+    m = masks[key]
+    m = m[:, c0:c0 + (x.shape[1] if c is None else c)].to(x.device)
+    return torch.where(m, x, 0.2 * x)
 
 
-def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
+def forward(P, inp, n_frames=2, large=False, taps=None, pre=None, masks=None):
     """HRNet.forward (nets/HRNet.py:524-601) for syn_type 'inter' (and 'extra' without
     inpainting).  inp: (B, 3F + 20F, H, W).  Returns (rgb, seg_logits).  pre: VAEHRNet's
-    decoded feature, leading the stem concat (HRNet.py:997)."""
+    decoded feature, leading the stem concat (HRNet.py:997).  masks: imposed LeakyReLU
+    branches (see _lrelu), keyed by the HRNet plan's activation buffer names."""
+    M = masks
     F_ = n_frames
     segs = [inp[:, 3 * F_ + 20 * k: 3 * F_ + 20 * (k + 1)] for k in range(F_)]
     enc = []
@@ -103,14 +117,14 @@ def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
         h = F.elu(_conv(P, "seg_encoder.2", h))
         enc.append(_conv(P, "seg_encoder.4", h))
     x = torch.cat(([pre] if pre is not None else []) + [inp[:, :3 * F_]] + enc, 1)
-    x = _lrelu(_conv(P, "conv1", x))
-    x = _lrelu(_conv(P, "conv2", x))
+    x = _lrelu(_conv(P, "conv1", x), M, "stem1")
+    x = _lrelu(_conv(P, "conv2", x), M, "stem2")
     for b in range(4):  # Bottleneck (l.66-85)
         r = _conv(P, "layer1.0.downsample.0", x) if b == 0 else x
-        o = _lrelu(_conv(P, f"layer1.{b}.conv1", x))
-        o = _lrelu(_conv(P, f"layer1.{b}.conv2", o))
+        o = _lrelu(_conv(P, f"layer1.{b}.conv1", x), M, f"layer1.{b}.a")
+        o = _lrelu(_conv(P, f"layer1.{b}.conv2", o), M, f"layer1.{b}.b")
         o = _conv(P, f"layer1.{b}.conv3", o)
-        x = _lrelu(o + r)
+        x = _lrelu(o + r, M, f"layer1.{b}.out")
     y_list = [x]
     pre = [256]
     for si, chans in enumerate(STAGES[large]):
@@ -120,13 +134,13 @@ def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
             src = x if si == 0 else y_list[-1]
             if i < len(pre):
                 if c != pre[i]:
-                    x_list.append(_lrelu(_conv(P, f"{t}.{i}.0", src)))
+                    x_list.append(_lrelu(_conv(P, f"{t}.{i}.0", src), M, f"trans{si}.{i}.0"))
                 else:
                     x_list.append(y_list[i])
             else:
                 h = src
                 for j in range(i + 1 - len(pre)):
-                    h = _lrelu(_conv(P, f"{t}.{i}.{j}.0", h, s=2))
+                    h = _lrelu(_conv(P, f"{t}.{i}.{j}.0", h, s=2), M, f"trans{si}.{i}.{j}")
                 x_list.append(h)
         st = f"stage{si + 2}.0"
         nb = len(chans)
@@ -134,11 +148,11 @@ def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
         for i in range(nb):  # BasicBlock (l.28-44)
             h = x_list[i]
             for b in range(4):
-                o = _lrelu(_conv(P, f"{st}.branches.{i}.{b}.conv1", h))
+                o = _lrelu(_conv(P, f"{st}.branches.{i}.{b}.conv1", h), M, f"{st}.branches.{i}.{b}.h")
                 if taps is not None:
                     taps[f"{st}.branches.{i}.{b}.h"] = o
                 o = _conv(P, f"{st}.branches.{i}.{b}.conv2", o)
-                h = _lrelu(o + h)
+                h = _lrelu(o + h, M, f"{st}.branches.{i}.{b}.out")
                 if taps is not None:
                     taps[f"{st}.branches.{i}.{b}.out"] = h
             xs.append(h)
@@ -147,7 +161,7 @@ def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
             if i == 0:
                 y = xs[0]
             else:
-                y = _fuse_down(P, st, i, 0, xs[0])
+                y = _fuse_down(P, st, i, 0, xs[0], M)
             for j in range(1, nb):
                 if i == j:
                     y = y + xs[j]
@@ -156,22 +170,28 @@ def forward(P, inp, n_frames=2, large=False, taps=None, pre=None):
                                           size=[xs[i].shape[-2], xs[i].shape[-1]], mode="bilinear",
                                           align_corners=False)
                 else:
-                    y = y + _fuse_down(P, st, i, j, xs[j])
-            ys.append(_lrelu(y))
+                    y = y + _fuse_down(P, st, i, j, xs[j], M)
+            final = si == len(STAGES[large]) - 1
+            # the plan writes the final stage's first fuse output into the concat buffer
+            ys.append(_lrelu(y, M, ("cat", 0, y.shape[1]) if final and i == 0 else f"{st}.y{i}"))
         y_list = ys
         pre = chans
     x = y_list
     h0, w0 = x[0].shape[-2:]
     ups = [F.interpolate(t, size=(h0, w0), mode="bilinear", align_corners=False) for t in x[1:]]
     x = torch.cat([x[0]] + ups, 1)
-    rgb = _conv(P, "rgb_layer.2", _lrelu(_conv(P, "rgb_layer.0", x)))
-    seg = _conv(P, "seg_layer.2", _lrelu(_conv(P, "seg_layer.0", x)))
+    last = x.shape[1]
+    stacked = M is not None and "heads_hidden" in M  # the plan's stacked 448 -> 896 head conv
+    rgb = _conv(P, "rgb_layer.2", _lrelu(_conv(P, "rgb_layer.0", x), M,
+                                         ("heads_hidden", 0, last) if stacked else "rgb_hidden"))
+    seg = _conv(P, "seg_layer.2", _lrelu(_conv(P, "seg_layer.0", x), M,
+                                         ("heads_hidden", last, last) if stacked else "seg_hidden"))
     return rgb, seg
 
 
-def _fuse_down(P, st, i, j, x):
+def _fuse_down(P, st, i, j, x, masks=None):
     for k in range(i - j):
         x = _conv(P, f"{st}.fuse_layers.{i}.{j}.{k}.0", x, s=2)
         if k != i - j - 1:
-            x = _lrelu(x)
+            x = _lrelu(x, masks, f"{st}.down.{i}.{j}.{k}")
     return x

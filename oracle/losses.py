@@ -41,7 +41,7 @@ def gaussian_window(window_size=11, sigma=1.5):
 
 def ssim_value(img1, img2, window_size=11):
     c = img1.shape[1]
-    w = gaussian_window(window_size).expand(c, 1, window_size, window_size).contiguous()
+    w = gaussian_window(window_size).to(img1.dtype).expand(c, 1, window_size, window_size).contiguous()
     p = window_size // 2
     mu1 = F.conv2d(img1, w, padding=p, groups=c)
     mu2 = F.conv2d(img2, w, padding=p, groups=c)
@@ -84,8 +84,17 @@ def preprocess_norm(x):
     return (x - mean) / std
 
 
-def vgg_features(state, img):
-    """my_vgg.forward: relu1_2, relu2_2, relu3_4, relu4_4, relu5_4 with AvgPool2d(2,2)."""
+def _relu(x, masks, name):
+    """ReLU; with `masks` (plan buffer name -> bool NCHW tensor) the branch is imposed, as
+    hrnet._lrelu does for LeakyReLU (test support for fp64-vs-fp32 gradient checks)."""
+    if masks is None or name not in masks:
+        return F.relu(x)
+    return torch.where(masks[name][:, :x.shape[1]].to(x.device), x, torch.zeros_like(x))
+
+
+def vgg_features(state, img, masks=None):
+    """my_vgg.forward: relu1_2, relu2_2, relu3_4, relu4_4, relu5_4 with AvgPool2d(2,2).
+    masks: imposed ReLU branches keyed by the VGG plan's buffer names ('vgg<idx>')."""
     feats, x, idx = [], img, 0
     for v in VGG19_CFG:
         if v == "M":
@@ -94,17 +103,24 @@ def vgg_features(state, img):
             x = F.avg_pool2d(x, 2, 2)
             idx += 1
             continue
-        x = F.relu(F.conv2d(x, state[f"features.{idx}.weight"], state[f"features.{idx}.bias"], padding=1))
+        x = _relu(F.conv2d(x, state[f"features.{idx}.weight"], state[f"features.{idx}.bias"], padding=1), masks,
+                  f"vgg{idx}")
         idx += 2
         if idx in (4, 9, 18, 27, 36):
             feats.append(x)
     return feats
 
 
-def vgg_loss(state, a, b, normed=True):
+def _half(masks, lo, hi):
+    return None if masks is None else {k: v[lo:hi] for k, v in masks.items()}
+
+
+def vgg_loss(state, a, b, normed=True, masks=None):
+    """masks: the VGG loss plan's ReLU branches over its [a | b] batch (2B images)."""
     if not normed:
-        a, b = preprocess_norm(a), preprocess_norm(b)
-    fa, fb = vgg_features(state, a), vgg_features(state, b)
+        a, b = preprocess_norm(a).to(a.dtype), preprocess_norm(b).to(b.dtype)
+    n = a.shape[0]
+    fa, fb = vgg_features(state, a, _half(masks, 0, n)), vgg_features(state, b, _half(masks, n, 2 * n))
     return sum((x - y).abs().mean() for x, y in zip(fa, fb)) / len(fa)
 
 
@@ -124,12 +140,13 @@ def seg_ce(logits, onehot):
     return F.cross_entropy(logits, torch.argmax(onehot, dim=1))
 
 
-def rgb_loss(state, pred, gt, normed, w=(80.0, 80.0, 20.0, 20.0), prefix="coarse"):
-    """RGBLoss.forward (losses.py:223-241) with the default weights (options.py:122-141)."""
+def rgb_loss(state, pred, gt, normed, w=(80.0, 80.0, 20.0, 20.0), prefix="coarse", vmasks=None):
+    """RGBLoss.forward (losses.py:223-241) with the default weights (options.py:122-141).
+    vmasks: imposed VGG ReLU branches (see vgg_loss)."""
     return OrderedDict([
         (f"{prefix}_l1_loss", w[0] * l1_loss(pred, gt)),
         (f"{prefix}_gdl_loss", w[1] * gdl_loss(pred, gt)),
-        (f"{prefix}_vgg_loss", w[2] * vgg_loss(state, pred, gt, normed)),
+        (f"{prefix}_vgg_loss", w[2] * vgg_loss(state, pred, gt, normed, vmasks)),
         (f"{prefix}_ssim_loss", w[3] * ssim_loss(pred, gt)),
     ])
 

@@ -29,14 +29,19 @@ def synthetic_batch(n, H, W, first_index=0):
     return {k: torch.stack(v) for k, v in out.items()}
 
 
-def inter_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(80.0, 80.0, 20.0, 20.0, 30.0)):
-    """Returns (loss_dict values, grads dict, updated params, adamax state)."""
-    P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
+def inter_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(80.0, 80.0, 20.0, 20.0, 30.0),
+               masks=None, vmasks=None, dtype=torch.float32):
+    """Returns (loss_dict values, grads dict, updated params, adamax state).
+    Gradient checks of an implementation: dtype=torch.float64 with its activation branches
+    imposed (masks: HRNet LeakyReLUs, vmasks: VGG ReLUs; see hrnet._lrelu)."""
+    P = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in params.items()}
+    data = {k: v.to(dtype) for k, v in data.items()}
+    vgg_state = {k: v.to(dtype) for k, v in vgg_state.items()}
     gt_x, gt_seg = data["frame2"], data["seg2"]
     x = torch.cat([data["frame1"], data["frame3"]], 1)
     seg = torch.cat([data["seg1"], data["seg3"]], 1)
-    rgb, seg_out = hrnet.forward(P, torch.cat([x, seg], 1))
-    ld = losses.rgb_loss(vgg_state, rgb, gt_x, normed=False, w=weights[:4])
+    rgb, seg_out = hrnet.forward(P, torch.cat([x, seg], 1), masks=masks)
+    ld = losses.rgb_loss(vgg_state, rgb, gt_x, normed=False, w=weights[:4], vmasks=vmasks)
     ld["coarse_ce_loss"] = weights[4] * losses.seg_ce(seg_out, gt_seg)
     loss = 0
     for v in ld.values():
@@ -44,7 +49,7 @@ def inter_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(8
     ld["loss_all"] = loss
     (loss / world).backward()
     grads = {k: v.grad.detach().clone() for k, v in P.items()}
-    new, state = adamax(params, grads, lr, state)
+    new, state = adamax(params, {k: g.to(params[k].dtype) for k, g in grads.items()}, lr, state)
     return OrderedDict((k, float(v.detach())) for k, v in ld.items()), grads, new, state, (rgb.detach(), seg_out.detach())
 
 
@@ -62,7 +67,8 @@ def adamax(params, grads, lr, state=None, betas=(0.9, 0.999), eps=1e-8):
     return new, state
 
 
-def extra_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(80.0, 80.0, 20.0, 20.0, 30.0)):
+def extra_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(80.0, 80.0, 20.0, 20.0, 30.0),
+               **kw):
     """One ExtraTrainer step, num_pred_once = num_pred_step = 1 (reference
     runners/ExtraTrainer.py:249-323): x = cat(frame1, frame2), seg = cat(seg1, seg2),
     target frame3 / seg3; loss keys 'step_1_frame_1_coarse_*'.  With one predicted frame
@@ -70,7 +76,7 @@ def extra_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(8
     so the step is inter_step on the remapped sample."""
     remap = {"frame1": data["frame1"], "frame3": data["frame2"], "frame2": data["frame3"],
              "seg1": data["seg1"], "seg3": data["seg2"], "seg2": data["seg3"]}
-    ld, grads, new, state, outs = inter_step(params, vgg_state, remap, lr, world, state, weights)
+    ld, grads, new, state, outs = inter_step(params, vgg_state, remap, lr, world, state, weights, **kw)
     ren = OrderedDict()
     for k, v in ld.items():
         ren["step_1_frame_1_" + k if k.startswith("coarse") else k] = v
@@ -78,28 +84,37 @@ def extra_step(params, vgg_state, data, lr=1e-3, world=1, state=None, weights=(8
 
 
 def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats, lr=1e-3, disc_lr=1e-3,
-             w_rgb=(80.0, 80.0, 20.0, 20.0), w_ce=30.0, w_d=1.0, w_g=1.0, state=None):
+             w_rgb=(80.0, 80.0, 20.0, 20.0), w_ce=30.0, w_d=1.0, w_g=1.0, state=None, masks=None, vmasks=None,
+             gf_masks=None, gv_masks=None, dtype=torch.float32):
     """One InterGANTrainer step (reference runners/InterGANTrainer.py:359-456 with
     nets/InterGANNet.py:28-117), HRNet coarse model (mu = logvar = None, no KLD), frame and
     video discriminators with seg_disc.  Returns (loss dict, new generator params, new frame
-    disc params, new video disc params, states)."""
+    disc params, new video disc params, states).  Generator-gradient checks: dtype float64
+    with the implementation's activation branches imposed on every path into the generator
+    (masks: HRNet, vmasks: VGG, gf_masks / gv_masks: the frozen-discriminator G passes)."""
     from . import disc as D
-    P = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
-    Pf = {k: v.detach().clone().requires_grad_(True) for k, v in frame_p.items()}
-    Pv = {k: v.detach().clone().requires_grad_(True) for k, v in video_p.items()}
+    P = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in params.items()}
+    Pf = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in frame_p.items()}
+    Pv = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in video_p.items()}
+    data = {k: v.to(dtype) for k, v in data.items()}
+    vgg_state = {k: v.to(dtype) for k, v in vgg_state.items()}
+    frame_stats = {k: (m.to(dtype), v.to(dtype)) for k, (m, v) in frame_stats.items()}
+    video_stats = {k: (m.to(dtype), v.to(dtype)) for k, (m, v) in video_stats.items()}
     gt_x, gt_seg = data["frame2"], data["seg2"]
     x = torch.cat([data["frame1"], data["frame3"]], 1)
     seg = torch.cat([data["seg1"], data["seg3"]], 1)
-    rgb, seg_out = hrnet.forward(P, torch.cat([x, seg], 1))
+    rgb, seg_out = hrnet.forward(P, torch.cat([x, seg], 1), masks=masks)
     soft = torch.softmax(seg_out, dim=1)
     FS, VS = D.FRAME(23), D.VIDEO(23)
     df_fake = D.forward(Pf, FS, torch.cat([rgb.detach(), soft.detach()], 1), stats=frame_stats)
     df_real = D.forward(Pf, FS, torch.cat([gt_x, gt_seg], 1), stats=frame_stats)
     dv_fake = D.forward(Pv, VS, torch.cat([rgb.detach(), soft.detach(), x, seg], 1), stats=video_stats)
     dv_real = D.forward(Pv, VS, torch.cat([gt_x, gt_seg, x, seg], 1), stats=video_stats)
-    gf = D.forward({k: v.detach() for k, v in Pf.items()}, FS, torch.cat([rgb, soft], 1), stats=frame_stats)
-    gv = D.forward({k: v.detach() for k, v in Pv.items()}, VS, torch.cat([rgb, soft, x, seg], 1), stats=video_stats)
-    ld = losses.rgb_loss(vgg_state, (rgb + 1) / 2, (gt_x + 1) / 2, normed=False, w=w_rgb)
+    gf = D.forward({k: v.detach() for k, v in Pf.items()}, FS, torch.cat([rgb, soft], 1), stats=frame_stats,
+                   masks=gf_masks)
+    gv = D.forward({k: v.detach() for k, v in Pv.items()}, VS, torch.cat([rgb, soft, x, seg], 1), stats=video_stats,
+                   masks=gv_masks)
+    ld = losses.rgb_loss(vgg_state, (rgb + 1) / 2, (gt_x + 1) / 2, normed=False, w=w_rgb, vmasks=vmasks)
     ld["coarse_ce_loss"] = w_ce * losses.seg_ce(seg_out, gt_seg)
     ld["coarse_frame_loss"] = D.gan_scalar_loss(gf, w_g, True)
     ld["disc_frame_real_loss"] = D.gan_scalar_loss(df_real, w_d, True)
@@ -113,9 +128,11 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
     ld["loss_all"] = loss
     loss.backward()
     st = state or {}
-    new, st["g"] = adamax(params, {k: v.grad for k, v in P.items()}, lr, st.get("g"))
-    newf, st["f"] = D.adam_101(frame_p, {k: v.grad for k, v in Pf.items()}, disc_lr, st.get("f"))
-    newv, st["v"] = D.adam_101(video_p, {k: v.grad for k, v in Pv.items()}, disc_lr, st.get("v"))
+    new, st["g"] = adamax(params, {k: v.grad.to(params[k].dtype) for k, v in P.items()}, lr, st.get("g"))
+    newf, st["f"] = D.adam_101(frame_p, {k: v.grad.to(frame_p[k].dtype) for k, v in Pf.items()}, disc_lr,
+                               st.get("f"))
+    newv, st["v"] = D.adam_101(video_p, {k: v.grad.to(video_p[k].dtype) for k, v in Pv.items()}, disc_lr,
+                               st.get("v"))
     grads = {"g": {k: v.grad for k, v in P.items()}, "f": {k: v.grad for k, v in Pf.items()},
              "v": {k: v.grad for k, v in Pv.items()}}
     return OrderedDict((k, float(v)) for k, v in ld.items()), new, newf, newv, st, grads
