@@ -217,13 +217,13 @@ def test_hrnet_forward_fp32_parity(dev, monkeypatch):
 
 
 def test_hrnet_backward_fp32_parity(dev, monkeypatch):
-    """Parameter gradients vs an fp64 oracle's autograd.
+    """Parameter gradients vs an fp64 oracle's autograd on the same activation branches.
 
-    Metric: per-tensor relative L2 error.  A max-abs metric is ill-conditioned here: an
-    activation that fp64 puts at +1e-9 and fp32 at -1e-9 flips LeakyReLU's derivative
+    An activation that fp64 puts at +1e-9 and fp32 at -1e-9 flips LeakyReLU's derivative
     (1 vs 0.2) at that pixel, which moves single gradient entries by O(1) relative
-    (observed: 1 such flip in ~5e6 activations, |a| = 7.9e-9).  Tolerances: every
-    tensor < 2e-2 relative L2, median tensor < 1e-5 (fp32 rounding level)."""
+    (observed: 1 such flip in ~5e6 activations, |a| = 7.9e-9).  The fp64 oracle therefore
+    takes the branches the HIP forward took (Plan.activation_signs); what remains is fp32
+    rounding.  Metric: per-tensor relative L2.  Bars: every tensor <= 1e-4, median <= 1e-5."""
     m = _hrnet(dev, "fp32", monkeypatch)
     P0 = O.init_params(1024)
     x, seg = inputs.hrnet_input(2, 32, 64)
@@ -233,7 +233,8 @@ def test_hrnet_backward_fp32_parity(dev, monkeypatch):
     rgb, s = m(x.to(dev), seg.to(dev))
     ((rgb * w1.to(dev)).sum() + (s * w2.to(dev)).sum()).backward()
     P = {k: v.double().clone().requires_grad_(True) for k, v in P0.items()}
-    rr, sr = O.forward(P, torch.cat([x, seg], 1).double())
+    masks = m.coarse_model.last_plan.activation_signs()
+    rr, sr = O.forward(P, torch.cat([x, seg], 1).double(), masks=masks)
     ((rr * w1.double()).sum() + (sr * w2.double()).sum()).backward()
     named = dict(m.coarse_model.named_parameters())
     errs = {}
@@ -243,8 +244,8 @@ def test_hrnet_backward_fp32_parity(dev, monkeypatch):
     worst = max(errs, key=errs.get)
     med = float(np.median(list(errs.values())))
     print(f"grad rel-L2: median {med:.2e}, worst {errs[worst]:.2e} ({worst})")
-    assert errs[worst] < 2e-2, (worst, errs[worst])
-    assert med < 2e-3, med
+    assert errs[worst] <= 1e-4, (worst, errs[worst])
+    assert med <= 1e-5, med
 
 
 def test_hrnet_bf16_close_to_fp32(dev, monkeypatch):
