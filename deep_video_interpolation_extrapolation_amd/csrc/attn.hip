@@ -165,84 +165,364 @@ __global__ __launch_bounds__(256) void attn_corr_kernel(const dvie_attn_desc p) 
   epi1<T>(p, pix, j, s);
 }
 
-// ---- per-pixel row ops: one thread = one pixel ----
+// ---- per-pixel row ops: a group of 16 lanes per pixel (4 pixels per wave) ----
+// Lane l of a group handles the 4-element chunks l, l + 16, ... of the pixel's row (the
+// channels of a feature map, or the window weights), so the group's loads are one
+// contiguous run of the pixel's row; the row reductions are 16-lane xor shuffles.  A second
+// pass re-reads the row (L1-resident) to write the outputs.
+constexpr int RG = 16;
+
+__device__ __forceinline__ float grp_sum(float v) {
+  v += __shfl_xor(v, 8, RG);
+  v += __shfl_xor(v, 4, RG);
+  v += __shfl_xor(v, 2, RG);
+  v += __shfl_xor(v, 1, RG);
+  return v;
+}
+__device__ __forceinline__ float grp_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 8, RG));
+  v = fmaxf(v, __shfl_xor(v, 4, RG));
+  v = fmaxf(v, __shfl_xor(v, 2, RG));
+  v = fmaxf(v, __shfl_xor(v, 1, RG));
+  return v;
+}
+
+// 4 elements [e, e + 4) of a row with `len` valid entries: loads zero past len
+template <typename T>
+__device__ __forceinline__ f32x4 ld4(const T* row, int e, int len) {
+  if (e + 4 <= len) return V4<T>::load(row + e);
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < 4; ++k)
+    if (e + k < len) v[k] = ld1<T>(row + e + k);
+  return v;
+}
+
+// epilogue of a row chunk: entries past len are not written
+template <typename T>
+__device__ __forceinline__ void epi_chunk(const dvie_attn_desc& p, long long pix, int e, int len, f32x4 v) {
+  if (e + 4 <= len) {
+    epi4<T>(p, pix, e, v);
+  } else {
+    for (int k = 0; k < 4; ++k)
+      if (e + k < len) epi1<T>(p, pix, e + k, v[k]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void attn_row_kernel(const dvie_attn_desc p) {
-  const long long pix = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long pix = (long long)blockIdx.x * (256 / RG) + threadIdx.x / RG;
+  const int l = threadIdx.x % RG;
   const long long npx = (long long)p.n * p.h * p.w;
-  if (pix >= npx) return;
+  if (pix >= npx) return;  // whole groups leave together (the shuffles stay inside a group)
   const int K = p.wh * p.ww;
   const T* a = (const T*)p.a + pix * p.a_ld;
+  const T* b0 = p.b0 ? (const T*)p.b0 + pix * p.b_ld : nullptr;
+  const T* b1 = p.b1 ? (const T*)p.b1 + pix * p.b_ld : nullptr;
   switch (p.op) {
     case DVIE_ATTN_L2NORM: {
       float ss = 0.f;
-      for (int c = 0; c < p.c; ++c) {
-        const float t = ld1<T>(a + c);
-        ss += t * t;
+      for (int e = 4 * l; e < p.c; e += 4 * RG) {
+        const f32x4 v = ld4<T>(a, e, p.c);
+        ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
       }
-      const float r = sqrtf(ss);
-      for (int c = 0; c < p.c; ++c) epi1<T>(p, pix, c, ld1<T>(a + c) / r);
+      const float r = sqrtf(grp_sum(ss));
+      for (int e = 4 * l; e < p.c; e += 4 * RG) {
+        f32x4 v = ld4<T>(a, e, p.c);
+        for (int k = 0; k < 4; ++k) v[k] = v[k] / r;
+        epi_chunk<T>(p, pix, e, p.c, v);
+      }
       break;
     }
     case DVIE_ATTN_L2NORM_BWD: {
       // a = dL/dxn, b0 = xn, b1 = x:  dx = (a - xn <xn, a>) / |x|
-      const T* xn = (const T*)p.b0 + pix * p.b_ld;
-      const T* x = (const T*)p.b1 + pix * p.b_ld;
       float dot = 0.f, ss = 0.f;
-      for (int c = 0; c < p.c; ++c) {
-        const float t = ld1<T>(x + c);
-        dot += ld1<T>(xn + c) * ld1<T>(a + c);
-        ss += t * t;
+      for (int e = 4 * l; e < p.c; e += 4 * RG) {
+        const f32x4 g = ld4<T>(a, e, p.c), xn = ld4<T>(b0, e, p.c), x = ld4<T>(b1, e, p.c);
+        for (int k = 0; k < 4; ++k) {
+          dot += xn[k] * g[k];
+          ss += x[k] * x[k];
+        }
       }
-      const float r = sqrtf(ss);
-      for (int c = 0; c < p.c; ++c) epi1<T>(p, pix, c, (ld1<T>(a + c) - ld1<T>(xn + c) * dot) / r);
+      dot = grp_sum(dot);
+      const float r = sqrtf(grp_sum(ss));
+      for (int e = 4 * l; e < p.c; e += 4 * RG) {
+        const f32x4 g = ld4<T>(a, e, p.c), xn = ld4<T>(b0, e, p.c);
+        f32x4 v;
+        for (int k = 0; k < 4; ++k) v[k] = (g[k] - xn[k] * dot) / r;
+        epi_chunk<T>(p, pix, e, p.c, v);
+      }
       break;
     }
     case DVIE_ATTN_SOFTMAX: {
       const int J = p.nhalf * K;
       float mx = -INFINITY;
-      for (int j = 0; j < J; ++j) mx = fmaxf(mx, ld1<T>(a + j));
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        const f32x4 v = ld4<T>(a, e, J);
+        for (int k = 0; k < 4; ++k)
+          if (e + k < J) mx = fmaxf(mx, v[k]);
+      }
+      mx = grp_max(mx);
       float s = 0.f;
-      for (int j = 0; j < J; ++j) s += expf(ld1<T>(a + j) - mx);
-      const float inv = 1.f / s;
-      for (int j = 0; j < J; ++j) epi1<T>(p, pix, j, expf(ld1<T>(a + j) - mx) * inv);
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        const f32x4 v = ld4<T>(a, e, J);
+        for (int k = 0; k < 4; ++k)
+          if (e + k < J) s += expf(v[k] - mx);
+      }
+      const float inv = 1.f / grp_sum(s);
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        f32x4 v = ld4<T>(a, e, J);
+        for (int k = 0; k < 4; ++k) v[k] = expf(v[k] - mx) * inv;
+        epi_chunk<T>(p, pix, e, J, v);
+      }
       break;
     }
     case DVIE_ATTN_SOFTMAX_BWD: {
       // a = dL/dprob, b0 = prob: dz = prob * (a - <prob, a>)
       const int J = p.nhalf * K;
-      const T* pr = (const T*)p.b0 + pix * p.b_ld;
       float dot = 0.f;
-      for (int j = 0; j < J; ++j) dot += ld1<T>(pr + j) * ld1<T>(a + j);
-      for (int j = 0; j < J; ++j) epi1<T>(p, pix, j, ld1<T>(pr + j) * (ld1<T>(a + j) - dot));
-      break;
-    }
-    case DVIE_ATTN_WNORM: {
-      for (int m = 0; m < p.nhalf; ++m) {
-        float s = 0.f;
-        for (int k = 0; k < K; ++k) s += ld1<T>(a + m * K + k);
-        const float inv = 1.f / s;
-        for (int k = 0; k < K; ++k) epi1<T>(p, pix, m * K + k, ld1<T>(a + m * K + k) * inv);
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        const f32x4 g = ld4<T>(a, e, J), pr = ld4<T>(b0, e, J);
+        dot += pr[0] * g[0] + pr[1] * g[1] + pr[2] * g[2] + pr[3] * g[3];
+      }
+      dot = grp_sum(dot);
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        const f32x4 g = ld4<T>(a, e, J), pr = ld4<T>(b0, e, J);
+        f32x4 v;
+        for (int k = 0; k < 4; ++k) v[k] = pr[k] * (g[k] - dot);
+        epi_chunk<T>(p, pix, e, J, v);
       }
       break;
     }
+    case DVIE_ATTN_WNORM:
     case DVIE_ATTN_WNORM_BWD: {
-      // a = dL/dWn, b0 = Wn, b1 = W: per map dW = (a - <a, Wn>) / sum(W)
-      const T* wn = (const T*)p.b0 + pix * p.b_ld;
-      const T* w = (const T*)p.b1 + pix * p.b_ld;
-      for (int m = 0; m < p.nhalf; ++m) {
-        float dot = 0.f, s = 0.f;
-        for (int k = 0; k < K; ++k) {
-          dot += ld1<T>(a + m * K + k) * ld1<T>(wn + m * K + k);
-          s += ld1<T>(w + m * K + k);
+      // per map m (entries [m*K, (m+1)*K)): WNORM y = a / sum(a); WNORM_BWD (a = dL/dWn,
+      // b0 = Wn, b1 = W) y = (a - <a, Wn>) / sum(W)
+      const bool bwd = p.op == DVIE_ATTN_WNORM_BWD;
+      const int J = p.nhalf * K;
+      float s0 = 0.f, s1 = 0.f, d0 = 0.f, d1 = 0.f;
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        const f32x4 v = ld4<T>(bwd ? b1 : a, e, J);
+        f32x4 g = {0.f, 0.f, 0.f, 0.f}, wn = g;
+        if (bwd) {
+          g = ld4<T>(a, e, J);
+          wn = ld4<T>(b0, e, J);
         }
-        const float inv = 1.f / s;
-        for (int k = 0; k < K; ++k) epi1<T>(p, pix, m * K + k, (ld1<T>(a + m * K + k) - dot) * inv);
+        for (int k = 0; k < 4; ++k) {
+          const bool m0 = e + k < K;
+          (m0 ? s0 : s1) += v[k];
+          (m0 ? d0 : d1) += g[k] * wn[k];
+        }
+      }
+      const float inv0 = 1.f / grp_sum(s0), inv1 = 1.f / grp_sum(s1);
+      if (bwd) {
+        d0 = grp_sum(d0);
+        d1 = grp_sum(d1);
+      }
+      for (int e = 4 * l; e < J; e += 4 * RG) {
+        f32x4 v = ld4<T>(a, e, J);
+        for (int k = 0; k < 4; ++k) {
+          const bool m0 = e + k < K;
+          v[k] = (v[k] - (bwd ? (m0 ? d0 : d1) : 0.f)) * (m0 ? inv0 : inv1);
+        }
+        epi_chunk<T>(p, pix, e, J, v);
       }
       break;
     }
     default:
       break;
+  }
+}
+
+// ---- window ops on LDS tiles: one workgroup = a TP-pixel segment of one image row ----
+// The (wh x ww) window of every tile pixel reads the wh source rows around it over
+// TP + ww - 1 columns.  Channels go in chunks of CC; per (chunk, window row) the source row
+// segment (and, for the weighted gathers, that row's window weights) is staged in LDS, so
+// every source value is fetched from memory once per tile and re-read from LDS by the
+// ww (GATHER / CORR) window positions that use it.  LDS pixel stride CS = CC + 4 floats (an
+// odd multiple of 16 B: ds_read_b128 of consecutive pixels is conflict-free).
+constexpr int TP = 64, CC = 32, CS = CC + 4, WHX = 5, WWX = 9, SPAN = TP + WWX - 1;
+
+template <typename T>
+__device__ __forceinline__ void stage_row(float* dst, const T* base, long long ld, int n, int yy, int xs, int h, int w,
+                                          int c0, int c) {
+  // dst[px * CS + ch] = base[n, yy, xs + px, c0 + ch], zero outside the image / past c
+  const bool rowin = base && (unsigned)yy < (unsigned)h;
+  for (int e = threadIdx.x; e < SPAN * (CC / 4); e += 256) {
+    const int px = e / (CC / 4), q = e - px * (CC / 4);
+    const int x = xs + px, ch = c0 + 4 * q;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (rowin && (unsigned)x < (unsigned)w && ch < c) v = V4<T>::load(base + (((long long)n * h + yy) * w + x) * ld + ch);
+    *(f32x4*)(dst + px * CS + 4 * q) = v;
+  }
+}
+
+__device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3]; }
+
+struct Tile {
+  int n, y, x0;
+};
+__device__ __forceinline__ Tile tile_of(int w, int h) {
+  const int tx = cdiv(w, TP);
+  const long long r = blockIdx.x / tx;
+  Tile t;
+  t.x0 = (int)(blockIdx.x - r * tx) * TP;
+  t.y = (int)(r % h);
+  t.n = (int)(r / h);
+  return t;
+}
+
+// CORR: y[p, m*K + k] = <a[p, :c], b_m[p + o_k, :c]>.  Thread = (pixel px, pair group);
+// the (map, window column) pairs of each window row are spread over the 4 groups.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_corr_tile_kernel(const dvie_attn_desc p) {
+  __shared__ __attribute__((aligned(16))) float lds[TP * CS + 2 * SPAN * CS];
+  float* sA = lds;
+  float* sB = lds + TP * CS;
+  const Tile t = tile_of(p.w, p.h);
+  const int K = p.wh * p.ww, rh = p.wh / 2, rw = p.ww / 2, J = p.nhalf * K, NP = p.nhalf * p.ww;
+  const int px = threadIdx.x & (TP - 1), grp = threadIdx.x / TP;
+  const T* maps[2] = {(const T*)p.b0, (const T*)p.b1};
+  float acc[WHX][5];
+#pragma unroll
+  for (int r = 0; r < WHX; ++r)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[r][i] = 0.f;
+  for (int c0 = 0; c0 < p.c; c0 += CC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < TP * (CC / 4); e += 256) {  // this tile's a
+      const int q = e / (CC / 4), k = e - q * (CC / 4);
+      const int x = t.x0 + q, ch = c0 + 4 * k;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (x < p.w && ch < p.c) v = V4<T>::load((const T*)p.a + (((long long)t.n * p.h + t.y) * p.w + x) * p.a_ld + ch);
+      *(f32x4*)(sA + q * CS + 4 * k) = v;
+    }
+#pragma unroll
+    for (int r = 0; r < WHX; ++r) {
+      if (r < p.wh) {
+        if (r) __syncthreads();
+        for (int m = 0; m < p.nhalf; ++m)
+          stage_row<T>(sB + m * SPAN * CS, maps[m], p.b_ld, t.n, t.y + r - rh, t.x0 - rw, p.h, p.w, c0, p.c);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          const int pr = grp + 4 * i;
+          if (pr < NP) {
+            const int m = pr / p.ww, kc = pr - m * p.ww;
+            const float* bp = sB + m * SPAN * CS + (px + kc) * CS;
+            const float* ap = sA + px * CS;
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < CC / 4; ++q) s += dot4(*(const f32x4*)(ap + 4 * q), *(const f32x4*)(bp + 4 * q));
+            acc[r][i] += s;
+          }
+        }
+      }
+    }
+  }
+  // outputs through LDS so that consecutive lanes write consecutive entries of a pixel row
+  __syncthreads();
+  float* sO = lds;  // TP x J (J <= 2 * WHX * WWX = 90 < 2 * SPAN * CS / TP)
+#pragma unroll
+  for (int r = 0; r < WHX; ++r)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int pr = grp + 4 * i;
+      if (r < p.wh && pr < NP) {
+        const int m = pr / p.ww, kc = pr - m * p.ww;
+        sO[px * J + m * K + r * p.ww + kc] = maps[m] ? acc[r][i] : 0.f;
+      }
+    }
+  __syncthreads();
+  const int npx = min(TP, p.w - t.x0);
+  const long long pix0 = ((long long)t.n * p.h + t.y) * p.w + t.x0;
+  for (int e = threadIdx.x; e < npx * J; e += 256) {
+    const int q = e / J, j = e - q * J;
+    epi1<T>(p, pix0 + q, j, sO[q * J + j]);
+  }
+}
+
+// GATHER: y[p, :c] = sum_m sum_k a[p, (half0 + m) K + k] * b_m[p + o_k, :c];
+// thread = (pixel, 8 channels of the chunk)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_gather_tile_kernel(const dvie_attn_desc p) {
+  constexpr int WS = 2 * WWX + 1;  // per-pixel weights of one window row (both maps), odd stride
+  __shared__ __attribute__((aligned(16))) float sB[2 * SPAN * CS];
+  __shared__ float sW[TP * WS];
+  const Tile t = tile_of(p.w, p.h);
+  const int K = p.wh * p.ww, rh = p.wh / 2, rw = p.ww / 2;
+  const int nm = p.b1 ? 2 : 1;
+  const int px = threadIdx.x & (TP - 1), cg = threadIdx.x / TP;
+  const T* maps[2] = {(const T*)p.b0, (const T*)p.b1};
+  const long long pix0 = ((long long)t.n * p.h + t.y) * p.w + t.x0;
+  const int npx = min(TP, p.w - t.x0);
+  for (int c0 = 0; c0 < p.c; c0 += CC) {
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    for (int r = 0; r < p.wh; ++r) {
+      __syncthreads();
+      for (int m = 0; m < nm; ++m)
+        stage_row<T>(sB + m * SPAN * CS, maps[m], p.b_ld, t.n, t.y + r - rh, t.x0 - rw, p.h, p.w, c0, p.c);
+      for (int e = threadIdx.x; e < TP * nm * p.ww; e += 256) {
+        const int q = e / (nm * p.ww), mk = e - q * (nm * p.ww);
+        const int m = mk / p.ww, kc = mk - m * p.ww;
+        sW[q * WS + mk] = q < npx ? ld1<T>((const T*)p.a + (pix0 + q) * p.a_ld + (p.half0 + m) * K + r * p.ww + kc) : 0.f;
+      }
+      __syncthreads();
+      for (int m = 0; m < nm; ++m)
+        for (int kc = 0; kc < p.ww; ++kc) {
+          const float wk = sW[px * WS + m * p.ww + kc];
+          const float* bp = sB + m * SPAN * CS + (px + kc) * CS + 8 * cg;
+          acc0 += wk * *(const f32x4*)bp;
+          acc1 += wk * *(const f32x4*)(bp + 4);
+        }
+    }
+    const int ch = c0 + 8 * cg;
+    if (px < npx) {
+      if (ch < p.c) epi4<T>(p, pix0 + px, ch, acc0);
+      if (ch + 4 < p.c) epi4<T>(p, pix0 + px, ch + 4, acc1);
+    }
+  }
+}
+
+// GATHER_T: y[q, :c] = sum_k a[q - o_k, half0 K + k] * b0[q - o_k, :c] (the adjoint of GATHER
+// in b); staged source row r holds y + r - rh, whose window entries for q are k = (wh-1-r) ww + kc
+template <typename T>
+__global__ __launch_bounds__(256) void attn_gather_t_tile_kernel(const dvie_attn_desc p) {
+  __shared__ __attribute__((aligned(16))) float sB[SPAN * CS];
+  __shared__ float sW[SPAN * WWX];
+  const Tile t = tile_of(p.w, p.h);
+  const int K = p.wh * p.ww, rh = p.wh / 2, rw = p.ww / 2;
+  const int px = threadIdx.x & (TP - 1), cg = threadIdx.x / TP;
+  const long long pix0 = ((long long)t.n * p.h + t.y) * p.w + t.x0;
+  const int npx = min(TP, p.w - t.x0);
+  const int span = TP + p.ww - 1;
+  for (int c0 = 0; c0 < p.c; c0 += CC) {
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    for (int r = 0; r < p.wh; ++r) {
+      const int yy = t.y + r - rh, kr = p.wh - 1 - r;
+      __syncthreads();
+      stage_row<T>(sB, (const T*)p.b0, p.b_ld, t.n, yy, t.x0 - rw, p.h, p.w, c0, p.c);
+      for (int e = threadIdx.x; e < span * p.ww; e += 256) {
+        const int s = e / p.ww, kc = e - s * p.ww;
+        const int x = t.x0 - rw + s;
+        float v = 0.f;
+        if ((unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w)
+          v = ld1<T>((const T*)p.a + (((long long)t.n * p.h + yy) * p.w + x) * p.a_ld + p.half0 * K + kr * p.ww + kc);
+        sW[s * WWX + kc] = v;
+      }
+      __syncthreads();
+      for (int kc = 0; kc < p.ww; ++kc) {
+        const int s = px + p.ww - 1 - kc;
+        const float wk = sW[s * WWX + kc];
+        const float* bp = sB + s * CS + 8 * cg;
+        acc0 += wk * *(const f32x4*)bp;
+        acc1 += wk * *(const f32x4*)(bp + 4);
+      }
+    }
+    const int ch = c0 + 8 * cg;
+    if (px < npx) {
+      if (ch < p.c) epi4<T>(p, pix0 + px, ch, acc0);
+      if (ch + 4 < p.c) epi4<T>(p, pix0 + px, ch + 4, acc1);
+    }
   }
 }
 
@@ -257,49 +537,84 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
                  d->wh, d->ww);
   DVIE_CHECK_ARG(d->dtype == DVIE_F32 || d->dtype == DVIE_BF16, "attn: dtype");
   DVIE_CHECK_ARG(!d->dact || d->z, "attn: dact needs z");
+  DVIE_CHECK_ARG(d->a_ld % 4 == 0 && d->y_ld % 4 == 0 && ((!d->b0 && !d->b1) || d->b_ld % 4 == 0) &&
+                     (!d->res || d->res_ld % 4 == 0) && (!d->z || d->z_ld % 4 == 0),
+                 "attn: every ld must be a multiple of 4");
   const int K = d->wh * d->ww;
   const long long npx = (long long)d->n * d->h * d->w;
-  const bool vec = d->op == DVIE_ATTN_GATHER || d->op == DVIE_ATTN_GATHER_T || d->op == DVIE_ATTN_POOL ||
-                   d->op == DVIE_ATTN_POOL_T;
+  const bool bf = d->dtype == DVIE_BF16;
   hipStream_t s = (hipStream_t)stream;
-  if (vec) {
-    DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0, "attn: c=%d must be a multiple of 4", d->c);
-    DVIE_CHECK_ARG(d->y_ld % 4 == 0 && d->b_ld % 4 == 0 && d->a_ld % 4 == 0 && (!d->res || d->res_ld % 4 == 0) &&
-                       (!d->z || d->z_ld % 4 == 0),
-                   "attn: ld alignment");
-    if (d->op == DVIE_ATTN_GATHER || d->op == DVIE_ATTN_GATHER_T) {
-      DVIE_CHECK_ARG(d->b0, "attn: gather needs b0");
-      DVIE_CHECK_ARG(d->half0 >= 0 && d->half0 + (d->b1 ? 2 : 1) <= d->nhalf && d->a_ld >= d->nhalf * K,
-                     "attn: gather half0=%d nhalf=%d", d->half0, d->nhalf);
+  // the LDS-tiled window kernels cover windows up to WHX x WWX (the refinement nets' 5 x 9)
+  const bool tiled = d->wh <= WHX && d->ww <= WWX;
+  const long long tiles = (long long)d->n * d->h * cdiv(d->w, TP);
+  switch (d->op) {
+    case DVIE_ATTN_GATHER:
+    case DVIE_ATTN_GATHER_T:
+    case DVIE_ATTN_POOL:
+    case DVIE_ATTN_POOL_T: {
+      DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0, "attn: c=%d must be a multiple of 4", d->c);
+      if (d->op == DVIE_ATTN_GATHER || d->op == DVIE_ATTN_GATHER_T) {
+        DVIE_CHECK_ARG(d->b0, "attn: gather needs b0");
+        DVIE_CHECK_ARG(d->half0 >= 0 && d->half0 + (d->b1 ? 2 : 1) <= d->nhalf && d->a_ld >= d->nhalf * K,
+                       "attn: gather half0=%d nhalf=%d", d->half0, d->nhalf);
+        DVIE_CHECK_ARG(d->op == DVIE_ATTN_GATHER || !d->b1, "attn: gather_t takes one map");
+      }
+      if (tiled && d->op == DVIE_ATTN_GATHER) {
+        if (bf)
+          hipLaunchKernelGGL(attn_gather_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        else
+          hipLaunchKernelGGL(attn_gather_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        break;
+      }
+      if (tiled && d->op == DVIE_ATTN_GATHER_T) {
+        if (bf)
+          hipLaunchKernelGGL(attn_gather_t_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        else
+          hipLaunchKernelGGL(attn_gather_t_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        break;
+      }
+      const long long tot = npx * (d->c / 4);
+      const dim3 grid((unsigned)((tot + 255) / 256));
+      if (bf)
+        hipLaunchKernelGGL(attn_vec_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+      else
+        hipLaunchKernelGGL(attn_vec_kernel<float>, grid, dim3(256), 0, s, *d);
+      break;
     }
-    const long long tot = npx * (d->c / 4);
-    const dim3 grid((unsigned)((tot + 255) / 256));
-    if (d->dtype == DVIE_BF16)
-      hipLaunchKernelGGL(attn_vec_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
-    else
-      hipLaunchKernelGGL(attn_vec_kernel<float>, grid, dim3(256), 0, s, *d);
-  } else if (d->op == DVIE_ATTN_CORR) {
-    DVIE_CHECK_ARG((d->nhalf == 1 || d->nhalf == 2) && (d->b0 || d->b1), "attn: corr maps");
-    DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0 && d->a_ld % 4 == 0 && d->b_ld % 4 == 0, "attn: corr c=%d", d->c);
-    DVIE_CHECK_ARG(d->y_ld >= d->nhalf * K, "attn: corr y_ld");
-    const long long tot = npx * d->nhalf * K;
-    const dim3 grid((unsigned)((tot + 255) / 256));
-    if (d->dtype == DVIE_BF16)
-      hipLaunchKernelGGL(attn_corr_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
-    else
-      hipLaunchKernelGGL(attn_corr_kernel<float>, grid, dim3(256), 0, s, *d);
-  } else {
-    DVIE_CHECK_ARG(d->op == DVIE_ATTN_L2NORM || d->op == DVIE_ATTN_L2NORM_BWD || d->op == DVIE_ATTN_SOFTMAX ||
-                       d->op == DVIE_ATTN_SOFTMAX_BWD || d->op == DVIE_ATTN_WNORM || d->op == DVIE_ATTN_WNORM_BWD,
-                   "attn: unknown op %d", d->op);
-    if (d->op == DVIE_ATTN_L2NORM_BWD || d->op == DVIE_ATTN_WNORM_BWD)
-      DVIE_CHECK_ARG(d->b0 && d->b1, "attn: backward needs b0 and b1");
-    if (d->op == DVIE_ATTN_SOFTMAX_BWD) DVIE_CHECK_ARG(d->b0, "attn: softmax backward needs b0");
-    const dim3 grid((unsigned)((npx + 255) / 256));
-    if (d->dtype == DVIE_BF16)
-      hipLaunchKernelGGL(attn_row_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
-    else
-      hipLaunchKernelGGL(attn_row_kernel<float>, grid, dim3(256), 0, s, *d);
+    case DVIE_ATTN_CORR: {
+      DVIE_CHECK_ARG((d->nhalf == 1 || d->nhalf == 2) && (d->b0 || d->b1), "attn: corr maps");
+      DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0, "attn: corr c=%d", d->c);
+      DVIE_CHECK_ARG(d->y_ld >= d->nhalf * K, "attn: corr y_ld");
+      if (tiled) {
+        if (bf)
+          hipLaunchKernelGGL(attn_corr_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        else
+          hipLaunchKernelGGL(attn_corr_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        break;
+      }
+      const long long tot = npx * d->nhalf * K;
+      const dim3 grid((unsigned)((tot + 255) / 256));
+      if (bf)
+        hipLaunchKernelGGL(attn_corr_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+      else
+        hipLaunchKernelGGL(attn_corr_kernel<float>, grid, dim3(256), 0, s, *d);
+      break;
+    }
+    default: {
+      DVIE_CHECK_ARG(d->op == DVIE_ATTN_L2NORM || d->op == DVIE_ATTN_L2NORM_BWD || d->op == DVIE_ATTN_SOFTMAX ||
+                         d->op == DVIE_ATTN_SOFTMAX_BWD || d->op == DVIE_ATTN_WNORM || d->op == DVIE_ATTN_WNORM_BWD,
+                     "attn: unknown op %d", d->op);
+      if (d->op == DVIE_ATTN_L2NORM_BWD || d->op == DVIE_ATTN_WNORM_BWD)
+        DVIE_CHECK_ARG(d->b0 && d->b1, "attn: backward needs b0 and b1");
+      if (d->op == DVIE_ATTN_SOFTMAX_BWD) DVIE_CHECK_ARG(d->b0, "attn: softmax backward needs b0");
+      if (d->op == DVIE_ATTN_WNORM || d->op == DVIE_ATTN_WNORM_BWD)
+        DVIE_CHECK_ARG(d->nhalf == 1 || d->nhalf == 2, "attn: wnorm takes one or two maps");
+      const dim3 grid((unsigned)((npx + (256 / RG) - 1) / (256 / RG)));
+      if (bf)
+        hipLaunchKernelGGL(attn_row_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+      else
+        hipLaunchKernelGGL(attn_row_kernel<float>, grid, dim3(256), 0, s, *d);
+    }
   }
   DVIE_RETURN_LAUNCH();
 }

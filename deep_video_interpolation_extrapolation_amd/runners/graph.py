@@ -11,9 +11,13 @@ and replays it: one launch per step, no Python or driver work per kernel.
 * Optimizers switch to their capturable form (device-resident step counts,
   optim._FusedOptimizer.set_capturable), so bias corrections advance on replay.
 * W == 1: the whole step is one graph.  W > 1: collectives are not captured; graph 1 =
-  forward + backward (in-backward bucket all-reduces off), then the eager RCCL all-reduce
-  of the flat gradients (GradSync.reduce), then graph 2 = 1/W scale + optimizer steps, then
-  the eager loss-value all-reduce.
+  forward + backward, in which every gradient bucket the eager backward would all-reduce
+  in flight (runners/comm.py) ends with an external event-record node instead; on replay
+  each bucket's RCCL all-reduce is issued on a communication stream waiting for its event
+  (GradSync.reduce_replayed), so it overlaps the rest of the replayed backward as the eager
+  step's does; then graph 2 = 1/W scale + optimizer steps, then the eager loss-value
+  all-reduce.  (A step whose backward accumulates twice -- ExtraTrainer's rollout --
+  records no bucket events: its flat gradients are reduced after graph 1.)
 * The warm-up steps before capture (on a side stream, as stream capture requires) are real
   training steps; capture itself executes nothing.
 """
@@ -31,12 +35,10 @@ class GraphedStep:
         dev = trainer.device
         self.inputs = {k: v.to(dev).clone() for k, v in example.items()}
         self.split = trainer.W > 1
+        self.events = []
         opts = trainer._opts()
         for o in opts:
             o.set_capturable(True)
-        if self.split:
-            trainer.model.set_overlap(False)  # no collectives inside the captured backward
-            trainer.no_overlap = True
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -52,8 +54,13 @@ class GraphedStep:
             self.graphs = (self.graph,)
         else:
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self.out = trainer.forward_backward(self.inputs)
+            trainer.model.capture_events = []  # bucket hooks record events, launch nothing
+            try:
+                with torch.cuda.graph(self.graph):
+                    self.out = trainer.forward_backward(self.inputs)
+            finally:
+                self.events = trainer.model.capture_events
+                trainer.model.capture_events = None
             self.graph2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph2, pool=self.graph.pool()):
                 trainer.apply_gradients(reduce=False)
@@ -62,15 +69,12 @@ class GraphedStep:
 
     def close(self):
         """Give the trainer back its eager form: optimizers leave capturable mode (step counts
-        return to the host, as checkpoints store them) and, at W > 1, the in-backward bucket
-        all-reduces are on again.  The captured graphs are released."""
+        return to the host, as checkpoints store them).  The captured graphs are released."""
         tr = self.tr
         for o in tr._opts():
             o.set_capturable(False)
-        if self.split:
-            tr.no_overlap = False
-            tr.model.set_overlap(True)
         self.graph = self.graph2 = None
+        self.events = []
         self.graphs = ()
 
     def __enter__(self):
@@ -96,7 +100,7 @@ class GraphedStep:
         if not self.split:
             tr.global_step += 1
             return self.out
-        tr.model.reduce()
+        tr.model.reduce_replayed(self.events)
         self.graph2.replay()
         tr.global_step += 1
         return comm.sync_losses(OrderedDict((k, v.clone()) for k, v in self.out.items()), tr.W)

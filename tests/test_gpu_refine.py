@@ -33,14 +33,9 @@ def _args(**kw):
     return a
 
 
-@pytest.mark.parametrize("prop", [False, True])
-def test_attention_ops_match_oracle(dev, prop):
-    """l2norm -> corr -> softmax (-> pool) -> gather / wnorm + per-map gather, fp32, vs the
-    oracle's corrmap / weighted_neighbours / weighted_neighbours_low in fp64: outputs 1e-5,
-    input gradients 1e-4 relative L2."""
+def _attn_graph(dtype, B, C, H, W, prop):
     from deep_video_interpolation_extrapolation_amd import engine as E
-    B, C, H, W = 2, 16, 7, 12
-    g = E.Graph(torch.float32)
+    g = E.Graph(dtype)
     X = {k: g.buffer(k, H, W, C) for k in ("x", "t1", "t2")}
     for k, b in X.items():
         g.input_nchw(E.R(b), k, ext_c=C, requires_grad=True)
@@ -65,6 +60,11 @@ def test_attention_ops_match_oracle(dev, prop):
     g.gather(E.R(wn), [E.R(X["t2"])], E.R(lb), 1, 2, 5, 9)
     for k, b in (("out", out), ("lf", lf), ("lb", lb)):
         g.output_nchw(k, E.R(b), C)
+    return g, X
+
+
+def _run_attn(dev, dtype, B, C, H, W, prop):
+    g, X = _attn_graph(dtype, B, C, H, W, prop)
     plan = g.compile(B, dev, backward=True)
     gen = torch.Generator().manual_seed(4)
     ins = {k: torch.randn((B, C, H, W), generator=gen) for k in X}
@@ -85,16 +85,43 @@ def test_attention_ops_match_oracle(dev, prop):
         plan.set_input_grad(k, t)
     plan.run_backward()
     torch.cuda.synchronize()
+    return ins, gouts, {k: t.cpu() for k, t in outs.items()}, {k: t.cpu() for k, t in gin.items()}
 
+
+# (B, C, H, W): the small case, and one with several 32-channel chunks, several 64-pixel
+# row tiles, a ragged last tile and windows clipped at every border
+SHAPES = [(2, 16, 7, 12), (1, 128, 9, 150)]
+
+
+@pytest.mark.parametrize("prop", [False, True])
+@pytest.mark.parametrize("shape", SHAPES, ids=["small", "tiled"])
+def test_attention_ops_match_oracle(dev, prop, shape):
+    """l2norm -> corr -> softmax (-> pool) -> gather / wnorm + per-map gather, fp32, vs the
+    oracle's corrmap / weighted_neighbours / weighted_neighbours_low in fp64: outputs 1e-5,
+    input gradients 1e-4 relative L2."""
+    ins, gouts, outs, gin = _run_attn(dev, torch.float32, *shape, prop)
     r = {k: v.double().requires_grad_(True) for k, v in ins.items()}
     p, _ = OR.corrmap(r["x"], r["t1"], r["t2"], prop)
     ro = {"out": OR.weighted_neighbours(r["t1"], r["t2"], p)}
     ro["lf"], ro["lb"] = OR.weighted_neighbours_low(r["t1"], r["t2"], p)
     sum((ro[k] * gouts[k].double()).sum() for k in ro).backward()
     for k in ro:
-        assert float((outs[k].cpu().double() - ro[k].detach()).abs().max()) < 1e-5, k
+        assert float((outs[k].double() - ro[k].detach()).abs().max()) < 1e-5, k
     for k in r:
         assert rel_l2(gin[k], r[k].grad) < 1e-4, (k, rel_l2(gin[k], r[k].grad))
+
+
+@pytest.mark.parametrize("prop", [False, True])
+def test_attention_ops_bf16_close_to_fp32(dev, prop):
+    """The same attention chain in bf16 (the perf mode) against its fp32 run: outputs and
+    input gradients within 3e-2 relative L2 (bf16 storage of every intermediate)."""
+    shape = SHAPES[1]
+    _, _, o32, g32 = _run_attn(dev, torch.float32, *shape, prop)
+    _, _, o16, g16 = _run_attn(dev, torch.bfloat16, *shape, prop)
+    for k in o32:
+        assert rel_l2(o16[k], o32[k]) < 3e-2, (k, rel_l2(o16[k], o32[k]))
+    for k in g32:
+        assert torch.isfinite(g16[k]).all() and rel_l2(g16[k], g32[k]) < 3e-2, (k, rel_l2(g16[k], g32[k]))
 
 
 def _grads(P, names):
