@@ -172,11 +172,35 @@ def test_attn_refine_matches_oracle(dev, prop):
     sum((o * go).sum() for o, go in zip(ref, gos)).backward()
     for o, r in zip(outs, ref):
         assert float((o.detach().cpu() - r.detach()).abs().max()) < 1e-4
-    for f, rf in zip(flows, rflows):
-        assert f.shape == rf.shape and float((f.cpu() != rf).float().mean()) < 0.01
+    _check_flows(m, flows, rflows)
     named = dict(m.named_parameters())
     errs = [rel_l2(named[k].grad, P[k].grad) for k in P]
     assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (float(np.median(errs)), max(errs))
+
+
+def _check_flows(m, flows, rflows, tie=1e-4):
+    """Flow maps = per-map window argmax of the similarity.  Where the HIP argmax differs
+    from the oracle's, the two window entries must tie to fp32 rounding in the HIP
+    similarity buffer (near-collinear features at random init put several entries within
+    1e-6 of the maximum; the summation order decides those): gap <= 1e-4 (cosines)."""
+    from deep_video_interpolation_extrapolation_amd.nets.refine import WH, WW
+    for sim, f, rf in zip(m.last_plan.sims, flows, rflows):
+        assert f.shape == rf.shape
+        f, rf = f.cpu(), rf.cpu()
+        diff = (f != rf).any(2)  # (B, 2, h, w)
+        if not bool(diff.any()):
+            continue
+        s = sim.buf.t[..., :2 * WH * WW].float().cpu()  # (B, h, w, 2K)
+        n, h, w = s.shape[:3]
+        s = s.reshape(n, h, w, 2, WH * WW).permute(0, 3, 1, 2, 4)  # (B, 2, h, w, K)
+
+        def index(fl):
+            return ((fl[:, :, 0] + WW // 2) * WH + (fl[:, :, 1] + WH // 2)).long()
+
+        got = s.gather(-1, index(f).unsqueeze(-1))[..., 0]
+        want = s.gather(-1, index(rf).unsqueeze(-1))[..., 0]
+        gap = (got - want)[diff].abs()
+        assert float(gap.max()) <= tie, (int(diff.sum()), float(gap.max()))
 
 
 @pytest.mark.parametrize("stage3", [False, True])
