@@ -11,7 +11,6 @@ Gradient scaling follows the reference exactly: each rank back-propagates loss_a
 (the in-place div_ of `sync` is recorded by autograd) and DDP averages, so the applied
 gradient is (1/W) * mean_r grad(L_r); here: SUM all-reduce, then x 1/W.
 """
-import contextlib
 import os
 
 import torch
@@ -65,43 +64,42 @@ class GradSync:
             for m in self.hooked:
                 m.grad_hook = (self.bucket_bytes, self._make_hook(m)) if flag else None
 
-    # hipGraph capture of the backward (runners/graph.py): a list while capturing, into which
-    # the bucket hooks put (owner, lo, hi, event) -- the event an external event-record node
-    # of the captured graph -- instead of launching the all-reduce
-    capture_events = None
+    # hipGraph capture of the backward (runners/graph.py): while capturing, a callable
+    # fn(owner, lo, hi) the bucket hooks hand each finished bucket to (it closes the captured
+    # graph segment there) instead of launching the all-reduce
+    capture_cut = None
 
     def _make_hook(self, owner):
         def hook(lo, hi):
             if hi <= lo:
                 return
-            if self.capture_events is not None:
-                ev = None
-                if owner._flat_grad.is_cuda:
-                    ev = torch.cuda.Event(external=True)
-                    ev.record()
-                self.capture_events.append((owner, lo, hi, ev))
+            if self.capture_cut is not None:
+                self.capture_cut(owner, lo, hi)
                 return
             self.works.append(dist.all_reduce(owner._flat_grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
         return hook
 
-    def reduce_replayed(self, events):
-        """The collectives of a replayed backward graph: bucket k's all-reduce is issued on a
-        communication stream that waits for bucket k's event-record node, so it runs while
-        the graph's remaining backward kernels still execute (the overlap of the eager
-        in-backward buckets); then the post-backward owners' all-reduces; the current stream
-        waits for all of them."""
+    def reduce_bucket(self, owner, lo, hi):
+        """A replayed graph segment's finished bucket: its all-reduce on the communication
+        stream, ordered after the work enqueued so far on the current stream (the segment),
+        so it runs while the next segments replay."""
         if self.W == 1:
             return
-        if events:
-            cuda = events[0][0]._flat_grad.is_cuda  # (host tensors: the CPU gloo tests)
-            comm = self.comm_stream() if cuda else None
-            with torch.cuda.stream(comm) if cuda else contextlib.nullcontext():
-                for owner, lo, hi, ev in events:
-                    if ev is not None:
-                        comm.wait_event(ev)
-                    self.works.append(dist.all_reduce(owner._flat_grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
-        owners = self.post if events else self.flat_owners
-        for m in owners:
+        g = owner._flat_grad
+        if not g.is_cuda:  # host tensors (the CPU gloo tests)
+            self.works.append(dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+            return
+        comm = self.comm_stream()
+        comm.wait_stream(torch.cuda.current_stream(g.device))
+        with torch.cuda.stream(comm):
+            self.works.append(dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+
+    def reduce_rest(self, bucketed):
+        """After the replayed backward: the all-reduces not issued per bucket (every flat
+        owner if no buckets were, else the post-backward owners), then wait for all."""
+        if self.W == 1:
+            return
+        for m in (self.post if bucketed else self.flat_owners):
             if m._flat_grad is not None and any(p.grad is not None for p in m.parameters()):
                 self.works.append(dist.all_reduce(m._flat_grad, op=dist.ReduceOp.SUM, async_op=True))
         self.wait()

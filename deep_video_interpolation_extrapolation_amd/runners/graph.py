@@ -10,14 +10,16 @@ and replays it: one launch per step, no Python or driver work per kernel.
   caller passes those tensors, `GraphedStep.inputs`, to skip the copy).
 * Optimizers switch to their capturable form (device-resident step counts,
   optim._FusedOptimizer.set_capturable), so bias corrections advance on replay.
-* W == 1: the whole step is one graph.  W > 1: collectives are not captured; graph 1 =
-  forward + backward, in which every gradient bucket the eager backward would all-reduce
-  in flight (runners/comm.py) ends with an external event-record node instead; on replay
-  each bucket's RCCL all-reduce is issued on a communication stream waiting for its event
-  (GradSync.reduce_replayed), so it overlaps the rest of the replayed backward as the eager
-  step's does; then graph 2 = 1/W scale + optimizer steps, then the eager loss-value
-  all-reduce.  (A step whose backward accumulates twice -- ExtraTrainer's rollout --
-  records no bucket events: its flat gradients are reduced after graph 1.)
+* W == 1: the whole step is one graph.  W > 1: collectives are not captured.  The
+  forward + backward is captured as a chain of graph segments that end where the eager
+  backward would launch a gradient bucket's all-reduce (runners/comm.py: the bucket hook
+  closes the segment and opens the next one on the capture stream); on replay, after each
+  segment its bucket's RCCL all-reduce is issued on a communication stream ordered after
+  that segment, so it overlaps the following segments as the eager in-backward buckets do;
+  then the remaining all-reduces and the wait (GradSync.reduce_rest), then graph 2 = 1/W
+  scale + optimizer steps, then the eager loss-value all-reduce.  (A step whose backward
+  accumulates twice -- ExtraTrainer's rollout -- has no buckets: one segment, then the
+  flat gradients' all-reduces.)
 * The warm-up steps before capture (on a side stream, as stream capture requires) are real
   training steps; capture itself executes nothing.
 """
@@ -35,7 +37,7 @@ class GraphedStep:
         dev = trainer.device
         self.inputs = {k: v.to(dev).clone() for k, v in example.items()}
         self.split = trainer.W > 1
-        self.events = []
+        self.segments = []
         opts = trainer._opts()
         for o in opts:
             o.set_capturable(True)
@@ -53,18 +55,34 @@ class GraphedStep:
                 self.out = trainer.step(self.inputs)
             self.graphs = (self.graph,)
         else:
-            self.graph = torch.cuda.CUDAGraph()
-            trainer.model.capture_events = []  # bucket hooks record events, launch nothing
-            try:
-                with torch.cuda.graph(self.graph):
+            pool = torch.cuda.graph_pool_handle()
+            self.segments = []  # [(graph, bucket (owner, lo, hi) finished at its end, or None)]
+            self._tick = torch.zeros(1, device=dev)
+            cur = [torch.cuda.CUDAGraph()]
+
+            def cut(owner, lo, hi):  # on the backward's thread and capture stream
+                cur[0].capture_end()
+                self.segments.append((cur[0], (owner, lo, hi)))
+                cur[0] = torch.cuda.CUDAGraph()
+                cur[0].capture_begin(pool=pool)
+
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(side):
+                cur[0].capture_begin(pool=pool)
+                trainer.model.capture_cut = cut
+                try:
                     self.out = trainer.forward_backward(self.inputs)
-            finally:
-                self.events = trainer.model.capture_events
-                trainer.model.capture_events = None
+                    self._tick.add_(1)  # the last segment is never empty
+                finally:
+                    trainer.model.capture_cut = None
+                    cur[0].capture_end()
+                self.segments.append((cur[0], None))
+            torch.cuda.current_stream(dev).wait_stream(side)
             self.graph2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph2, pool=self.graph.pool()):
+            with torch.cuda.graph(self.graph2, pool=pool):
                 trainer.apply_gradients(reduce=False)
-            self.graphs = (self.graph, self.graph2)
+            self.graph = self.segments[0][0]
+            self.graphs = tuple(g for g, _ in self.segments) + (self.graph2,)
         trainer.global_step = g0  # capture ran no step
 
     def close(self):
@@ -74,7 +92,7 @@ class GraphedStep:
         for o in tr._opts():
             o.set_capturable(False)
         self.graph = self.graph2 = None
-        self.events = []
+        self.segments = []
         self.graphs = ()
 
     def __enter__(self):
@@ -96,11 +114,15 @@ class GraphedStep:
                 if v.data_ptr() != t.data_ptr():
                     t.copy_(v, non_blocking=True)
         tr = self.tr
-        self.graph.replay()
         if not self.split:
+            self.graph.replay()
             tr.global_step += 1
             return self.out
-        tr.model.reduce_replayed(self.events)
+        for g, bucket in self.segments:
+            g.replay()
+            if bucket is not None:
+                tr.model.reduce_bucket(*bucket)
+        tr.model.reduce_rest(len(self.segments) > 1)
         self.graph2.replay()
         tr.global_step += 1
         return comm.sync_losses(OrderedDict((k, v.clone()) for k, v in self.out.items()), tr.W)

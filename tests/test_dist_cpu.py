@@ -73,22 +73,25 @@ def _worker(rank, world, port, q):
         dist.all_reduce(tot)
         assert torch.allclose(fg, tot, rtol=0, atol=1e-6), "bucketed all-reduce"
 
-        # graph-capture mode (runners/graph.py): the hooks record (owner, range) events in
-        # bucket order, launch nothing; the replay issues one all-reduce per recorded bucket,
-        # in the same order on every rank, then the post-backward owners
+        # graph-capture mode (runners/graph.py): the hooks hand each finished bucket to the
+        # capture's segment cut in bucket order and launch nothing; the replay issues one
+        # all-reduce per bucket, in the same order on every rank, then the rest
         fg.copy_(torch.randn(fg.shape, generator=gen))
         mine = fg.clone()
-        sync.capture_events = []
+        cutlist = []
+        sync.capture_cut = lambda owner, lo, hi: cutlist.append((owner, lo, hi))
         for lo, hi in ranges:
             hook(lo, hi)
-        events, sync.capture_events = sync.capture_events, None
-        assert [(lo, hi) for _, lo, hi, _ in events] == ranges and not sync.works
-        order = torch.tensor([x for _, lo, hi, _ in events for x in (lo, hi)])
+        sync.capture_cut = None
+        assert [(lo, hi) for _, lo, hi in cutlist] == ranges and not sync.works
+        order = torch.tensor([x for _, lo, hi in cutlist for x in (lo, hi)])
         orders = [torch.zeros_like(order) for _ in range(world)]
         dist.all_gather(orders, order)
         assert all(torch.equal(o, orders[0]) for o in orders), "bucket order differs across ranks"
         assert torch.equal(fg, mine), "capture mode launched a collective"
-        sync.reduce_replayed(events)
+        for bucket in cutlist:
+            sync.reduce_bucket(*bucket)
+        sync.reduce_rest(True)
         tot = mine.clone()
         dist.all_reduce(tot)
         assert torch.allclose(fg, tot, rtol=0, atol=1e-6), "replayed bucket all-reduce"

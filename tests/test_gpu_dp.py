@@ -121,8 +121,8 @@ def _dp_vs_single(dev, kind):
 
 def _graph_worker(rank, world, port, q):
     """Eager trainer A: 3 steps; trainer B: 2 eager warm-up steps + capture + 1 replay, its
-    gradient buckets all-reduced from the replayed graph's event nodes (GradSync.
-    reduce_replayed).  Both on the same shard, W = 2."""
+    gradient buckets all-reduced after the replayed graph segment that finishes them
+    (GradSync.reduce_bucket).  Both on the same shard, W = 2."""
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK="0", DVIE_PRECISION="fp32",
@@ -138,7 +138,7 @@ def _graph_worker(rank, world, port, q):
         la = [float(a.step(mine)["loss_all"]) for _ in range(3)]
         b = _trainer("inter", world, rank)
         gs = GraphedStep(b, mine, warmup=2)
-        nev = len(gs.events)
+        nev = len(gs.segments) - 1
         lb = float(gs.step()["loss_all"])
         torch.cuda.synchronize()
         ha, hb = a.model.module.coarse_model, b.model.module.coarse_model
@@ -152,8 +152,9 @@ def _graph_worker(rank, world, port, q):
 
 @pytest.mark.timeout(600)
 def test_graphed_dp2_step_overlaps_and_equals_eager(dev):
-    """The captured W = 2 step (bucket all-reduces issued per event node of the replayed
-    backward) gives the eager W = 2 step's gradients, parameters and logged loss."""
+    """The captured W = 2 step (a graph segment per gradient bucket, each bucket's
+    all-reduce issued behind its segment while the next ones replay) gives the eager W = 2
+    step's gradients, parameters and logged loss."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
