@@ -64,11 +64,12 @@ class GraphedStep:
                 cur[0].capture_end()
                 self.segments.append((cur[0], (owner, lo, hi)))
                 cur[0] = torch.cuda.CUDAGraph()
-                cur[0].capture_begin(pool=pool)
+                cur[0].capture_begin(pool=pool, capture_error_mode="relaxed")
 
             torch.cuda.synchronize(dev)
+            # relaxed capture: the segments end and begin on autograd's backward thread
             with torch.cuda.stream(side):
-                cur[0].capture_begin(pool=pool)
+                cur[0].capture_begin(pool=pool, capture_error_mode="relaxed")
                 trainer.model.capture_cut = cut
                 try:
                     self.out = trainer.forward_backward(self.inputs)
