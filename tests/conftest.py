@@ -40,3 +40,25 @@ def _test_local_env():
         if k not in saved:
             del os.environ[k]
     os.environ.update(saved)
+
+
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    """A line on stderr every 60 s while a test runs: the GPU box's runner takes a run that
+    writes nothing for 3 minutes to be hung, and some oracle evaluations (fp64 CPU passes of
+    a whole training step at 512x1024) take longer than that."""
+    import threading
+    import time
+    stop = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not stop.wait(60):
+            print(f"[heartbeat] {request.node.nodeid} running {time.time() - t0:.0f}s", file=sys.__stderr__,
+                  flush=True)
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    stop.set()
+    th.join(timeout=5)
