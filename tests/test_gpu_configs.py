@@ -15,7 +15,8 @@ is the checker only.  Tolerances as the 32x64 tests: loss dicts 1e-4 relative; g
 against the fp32 oracle by per-tensor relative L2 (median / worst), because an activation
 within rounding of zero may take the other LeakyReLU branch, and against the fp64 oracle
 evaluated on the HIP step's own activation branches (Plan.activation_signs imposed on every
-LeakyReLU / ReLU): every tensor within 1e-4 relative L2; first-step Adamax moves every
+LeakyReLU / ReLU): every tensor within 1e-4 relative L2 (C4: 3e-4, see there); first-step
+Adamax moves every
 weight by ~lr, so post-update weights are gated on the fraction of weights that differ.
 """
 import math
@@ -226,7 +227,10 @@ def test_c4_intergan_step_512x1024(dev):
     out64 = OS.gan_step(P, Pf, Pv, OL.synthetic_vgg19_state(), data, sf64, sv64, masks=masks, vmasks=vmasks,
                         gf_masks=m.frame_disc_model.activation_signs(),
                         gv_masks=m.video_disc_model.activation_signs(), dtype=torch.float64)
-    _check_grads_tight(named, out64[5]["g"], tag="C4")
+    # 3e-4 here: the generator gradient also comes back through the discriminators'
+    # train-mode BatchNorm backward (g - mean(g) - xhat * mean(g * xhat), cancelling in fp32
+    # over 512x1024 positions); measured (r03c) median 3.2e-5, worst 1.45e-4 (conv1.weight)
+    _check_grads_tight(named, out64[5]["g"], worst_bar=3e-4, tag="C4")
     del tr, m
     tb = _trainer("GAN", "bf16", 512, 1024, 2)
     ld = tb.step(OS.synthetic_batch(2, 512, 1024))

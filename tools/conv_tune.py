@@ -19,6 +19,8 @@ SHAPES = [  # name, cin, cout, k, H, W, batch
     ("3x3 128->128 128x256", 128, 128, 3, 128, 256, 8),
     ("3x3 256->256 64x128", 256, 256, 3, 64, 128, 8),
     ("1x1 448->448 256x512", 448, 448, 1, 256, 512, 8),
+    ("1x1 448->896 256x512", 448, 896, 1, 256, 512, 8),
+    ("1x1 896->448 256x512", 896, 448, 1, 256, 512, 8),
     ("3x3 448->8 256x512 f32out", 448, 8, 3, 256, 512, 8),
     ("3x3 448->24 256x512", 448, 24, 3, 256, 512, 8),
     ("3x3 256->64 256x512", 256, 64, 3, 256, 512, 8),
