@@ -376,8 +376,18 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
         __builtin_amdgcn_sched_barrier(0);
       }
       // everything issued before this step has landed (this step's loads may stay in flight;
-      // the epilogue prefetch, issued last, too)
-      wait_vmcnt(issued + (PRE && t == PRE_T && J.k + 1 == nchunks ? npre : 0));
+      // the epilogue prefetch, issued last, too).  Relaxed (epi_pre bit 2, default): the
+      // previous step's tail -- its share of the next job's halo and the epilogue prefetch,
+      // issued after its weights -- may stay in flight one more step (vmcnt is in order: the
+      // older weights of step sc+1 are still waited for), so those HBM/MALL loads get two
+      // steps of cover instead of one; at the job's last tap the halo must have landed.
+      const bool last = J.k + 1 == nchunks;
+      int allow = issued + (PRE && t == PRE_T && last ? npre : 0);
+      if (!kNT1 && (epi_pre & 4) && t > 0) {
+        const int pre_prev = PRE && t - 1 == PRE_T && last ? npre : 0;
+        allow += pre_prev + (t == C::NT - 1 ? 0 : C::q1(t - 1) - C::q0(t - 1));
+      }
+      wait_vmcnt(allow);
       // plain s_barrier: __syncthreads() would add a release fence, i.e. vmcnt(0)
       __builtin_amdgcn_s_barrier();
     }
@@ -491,6 +501,11 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
 // DVIE_EPI_PREFETCH=0: epilogue operands loaded in the epilogue (A/B runs)
 static const bool epi_prefetch_on = !(getenv("DVIE_EPI_PREFETCH") && *getenv("DVIE_EPI_PREFETCH") == '0');
 static const int halo_setprio = getenv("DVIE_SETPRIO") && *getenv("DVIE_SETPRIO") == '1' ? 2 : 0;
+// DVIE_HALO_WAIT=0: every step waits for all loads issued before it (A/B runs); read per launch
+static int halo_wait_flag() {
+  const char* e = getenv("DVIE_HALO_WAIT");
+  return e && *e == '0' ? 0 : 4;
+}
 
 template <int TM, int WC, int WP, int TH, int TW>
 static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
@@ -509,10 +524,10 @@ static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
     const int grid = persistent ? cap : n_tiles;
     if (p.out_f32)
       hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
-                         n_tiles, tiles_x, tiles_y, persistent, halo_setprio);
+                         n_tiles, tiles_x, tiles_y, persistent, halo_setprio | halo_wait_flag());
     else
       hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, false>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
-                         n_tiles, tiles_x, tiles_y, persistent, (epi_prefetch_on ? 1 : 0) | halo_setprio);
+                         n_tiles, tiles_x, tiles_y, persistent, (epi_prefetch_on ? 1 : 0) | halo_setprio | halo_wait_flag());
     return true;
   }
 }
