@@ -4,9 +4,10 @@
   C2  InterNet 256x512: fp32 HRNet forward vs the oracle (north-star bar 1e-3 max-abs);
       bf16 batch-8 step (the bench workload): finite gradients, and bf16 output quality
       against the fp32 CPU reference path (PSNR / SSIM, gated).
-  C3  ExtraNet int_9_len_3 256x512: fp32 step vs oracle.step.extra_step; bf16 batch-8 step.
+  C3  ExtraNet int_9_len_3 256x512: fp32 step vs oracle.step.extra_step; bf16 batch-8
+      outputs gated on PSNR / SSIM / seg agreement vs the fp32 CPU path, then a bf16 step.
   C4  InterGANTrainer (HRNet + FrameDisc + VideoDisc, VGG) 512x1024: fp32 step vs
-      oracle.step.gan_step; bf16 step finite.
+      oracle.step.gan_step; bf16 outputs gated as C3, then a bf16 step finite.
   C5  HRNet 1024x2048 (batch 1): fp32 forward vs the oracle (1e-3 max-abs), bf16 forward +
       backward finite with output PSNR vs fp32.
 
@@ -94,6 +95,29 @@ def _psnr01(a, b):
     """PSNR of two [-1, 1] images mapped to [0, 1] (losses.PSNR, losses.py:103-116)."""
     mse = float((((a + 1) / 2 - (b + 1) / 2) ** 2).mean())
     return 10 * math.log10(1.0 / max(mse, 1e-20))
+
+
+def _bf16_quality(tr, x, seg, idx, tag):
+    """bf16 coarse outputs of the trainer's HRNet against the fp32 CPU reference path on the
+    samples idx: RGB PSNR >= 40 dB and SSIM >= 0.99 (frames mapped to [0, 1]), seg argmax
+    agreement >= 99%, relative L2 < 2e-2 (the C2 gates)."""
+    cm = tr.model.module.coarse_model
+    dev = next(cm.parameters()).device
+    P = {k: v.detach().float().cpu() for k, v in cm.state_dict().items()}
+    psnrs, ssims, agree, rels = [], [], [], []
+    for i in idx:
+        with torch.no_grad():
+            rgb, s = cm.forward_split(x[i:i + 1].to(dev), seg[i:i + 1].to(dev))
+            rgb, s = rgb.float().cpu(), s.float().cpu()
+            rr, sr = O.forward(P, torch.cat([x[i:i + 1], seg[i:i + 1]], 1))
+        psnrs.append(_psnr01(rgb, rr))
+        ssims.append(float(OL.ssim_value((rgb + 1) / 2, (rr + 1) / 2)))
+        agree.append(float((s.argmax(1) == sr.argmax(1)).float().mean()))
+        rels.append(max(_rel_l2(rgb, rr), _rel_l2(s, sr)))
+    print(f"{tag} bf16 vs fp32 reference: PSNR {psnrs} dB, SSIM {ssims}, seg argmax agreement {agree}, "
+          f"relative L2 {rels}")
+    assert min(psnrs) >= 40.0 and min(ssims) >= 0.99 and min(agree) >= 0.99, (psnrs, ssims, agree)
+    assert max(rels) < 2e-2, rels
 
 
 def _all_finite(module):
@@ -185,7 +209,11 @@ def test_c3_extra_step_256x512(dev):
     _check_grads_tight(named, g64, tag="C3")
     del tr
     tb = _trainer("EXTRA", "bf16", 256, 512, 8)
-    ld = tb.step(OS.synthetic_batch(8, 256, 512))
+    data8 = OS.synthetic_batch(8, 256, 512)
+    x = torch.cat([data8["frame1"], data8["frame2"]], 1)
+    seg = torch.cat([data8["seg1"], data8["seg2"]], 1)
+    _bf16_quality(tb, x, seg, (0, 7), "C3")
+    ld = tb.step(data8)
     torch.cuda.synchronize()
     assert all(np.isfinite(float(v)) for v in ld.values()), ld
     assert _all_finite(tb.model.module.coarse_model)
@@ -233,7 +261,10 @@ def test_c4_intergan_step_512x1024(dev):
     _check_grads_tight(named, out64[5]["g"], worst_bar=3e-4, tag="C4")
     del tr, m
     tb = _trainer("GAN", "bf16", 512, 1024, 2)
-    ld = tb.step(OS.synthetic_batch(2, 512, 1024))
+    data2 = OS.synthetic_batch(2, 512, 1024)
+    _bf16_quality(tb, torch.cat([data2["frame1"], data2["frame3"]], 1),
+                  torch.cat([data2["seg1"], data2["seg3"]], 1), (0,), "C4")
+    ld = tb.step(data2)
     torch.cuda.synchronize()
     assert all(np.isfinite(float(v)) for v in ld.values()), ld
     for mod in (tb.model.module.coarse_model, tb.model.module.frame_disc_model, tb.model.module.video_disc_model):
