@@ -60,11 +60,14 @@ def report(path):
         fam = collections.Counter(family(r[key]) for r in seg)
         t = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg) / 1e6
         span = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e6 if seg else 0
-        native = {k: v for k, v in fam.items() if "at::native" in k or "at::" in k}
+        nat = [r for r in seg if "at::" in r[key]]
+        nt = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in nat) / 1e3
         print(f"replay: {len(seg)} kernels, busy {t:.3f} ms, span {span:.3f} ms; PyTorch-native kernels: "
-              f"{sum(native.values())} {dict(native)}")
+              f"{len(nat)} ({nt:.1f} us)")
         for k, v in fam.most_common():
             print(f"    {v:5d}  {k}")
+        for k, v in collections.Counter(re.sub(r", std::array.*|\(int,.*", "", r[key])[:160] for r in nat).most_common():
+            print(f"    native {v:3d}  {k}")
 
 
 if __name__ == "__main__":
