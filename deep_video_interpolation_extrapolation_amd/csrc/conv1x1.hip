@@ -616,151 +616,6 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Streaming form for one K-step (c <= 64) with identity output placement: the memory-bound
-// full-resolution layers (HRNet bottleneck expansion 64 -> 256 + residual + LeakyReLU, the
-// data gradients 64 -> 256 with identity / accumulate / activation-derivative epilogues).
-// Their time is the epilogue's HBM traffic (the output and up to three operand tensors of
-// 256 channels against a 64-channel input), so the kernel is built for loads in flight: the
-// weights (cout x 64) are staged in LDS once per workgroup, and every wave then walks its own
-// items (32 pixels x 32*TMC output channels) with no further barrier; per item it issues the
-// input fragments AND every epilogue operand of the item together, so their latencies
-// overlap, then runs 4*TMC MFMAs and the epilogue.  256-thread workgroups, several per CU.
-// EPI: bit 0 residual, bit 1 accumulate (beta), bit 2 activation derivative -- the operand
-// registers of an absent operand are not allocated.
-template <int TMC, int EPI>
-__global__ __launch_bounds__(256) void conv1x1s_kernel(const dvie_conv_desc p, int n_cg, long long n_items) {
-  __shared__ __attribute__((aligned(16))) char W[256 * 128];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int cout = p.cout;
-  const int rows = (cout + 31) & ~31;
-  for (int e = tid; e < rows * 8; e += 256) {  // weight rows (128 B), chunk ch at ch ^ swz(row)
-    const int row = e >> 3, ch = e & 7;
-    i32x4 v = {0, 0, 0, 0};
-    if (row < cout && ch * 8 < p.c) v = *(const i32x4*)((const bf16_t*)p.w + (long long)row * p.kpad + ch * 8);
-    *(i32x4*)(W + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4)) = v;
-  }
-  __syncthreads();
-  const long long npix = (long long)p.n * p.oh * p.ow;
-  const long long step = (long long)gridDim.x * 4;
-  const i32x4 Z = {0, 0, 0, 0};
-  for (long long it = (long long)blockIdx.x * 4 + wave; it < n_items; it += step) {
-    const int cg = (int)(it % n_cg);
-    const long long pix = (it / n_cg) * 32 + r32;
-    const bool pok = pix < npix;
-    const int co0 = cg * 32 * TMC;
-    // B fragments: x[pix][16 s + 8 hh .. +7]
-    i32x4 xb[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int ch = 16 * s + 8 * hh;
-      xb[s] = pok && ch < p.c ? *(const i32x4*)((const bf16_t*)p.x + pix * p.x_ld + ch) : Z;
-    }
-    // epilogue operands of the item, issued with the fragments: lane (pixel r32) channels
-    // co0 + 32 j + 16 P + 8 hh .. +7 (the accumulator layout after the permlane32 pairing)
-    i32x4 rr[(EPI & 1) ? TMC : 1][2], bb[(EPI & 2) ? TMC : 1][2], zz[(EPI & 4) ? TMC : 1][2];
-#pragma unroll
-    for (int j = 0; j < TMC; ++j)
-#pragma unroll
-      for (int P = 0; P < 2; ++P) {
-        const int co = co0 + 32 * j + 16 * P + 8 * hh;
-        const bool ok = pok && co < cout;
-        if constexpr ((EPI & 1) != 0) rr[j][P] = ok ? *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co) : Z;
-        if constexpr ((EPI & 2) != 0) bb[j][P] = ok ? *(const i32x4*)((const bf16_t*)p.y + pix * p.y_ld + co) : Z;
-        if constexpr ((EPI & 4) != 0) zz[j][P] = ok ? *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co) : Z;
-      }
-    f32x16 acc[TMC];
-#pragma unroll
-    for (int j = 0; j < TMC; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < TMC; ++j) {
-        const int row = co0 + 32 * j + r32;
-        const i32x4 a = *(const i32x4*)(W + row * 128 + (((2 * s + hh) ^ ((row >> 1) & 7)) << 4));
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, xb[s]),
-                                                         acc[j], 0, 0, 0);
-      }
-#pragma unroll
-    for (int j = 0; j < TMC; ++j) {
-      float v[2][8];
-#pragma unroll
-      for (int P = 0; P < 2; ++P)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[j][8 * P + e]),
-                                                           __float_as_uint(acc[j][8 * P + 4 + e]), false, false);
-          v[P][e] = __uint_as_float(sw[0]);
-          v[P][4 + e] = __uint_as_float(sw[1]);
-        }
-      if (!pok) continue;
-#pragma unroll
-      for (int P = 0; P < 2; ++P) {
-        const int co = co0 + 32 * j + 16 * P + 8 * hh;
-        if (co >= cout) continue;
-        float* w = v[P];
-        float t[8];
-        if (p.bias) {
-          const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            w[e] += b0[e];
-            w[4 + e] += b1[e];
-          }
-        }
-        if constexpr ((EPI & 1) != 0) {
-          unpack8(rr[j][P], t);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) w[e] += t[e];
-        }
-        if constexpr ((EPI & 2) != 0) {
-          unpack8(bb[j][P], t);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) w[e] += t[e];
-        }
-        act1(w, p.act, p.alpha);
-        if constexpr ((EPI & 4) != 0) {
-          unpack8(zz[j][P], t);
-          dact1(w, t, p.dact, p.alpha);
-        }
-        i32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (int)pk_bf16(w[2 * e], w[2 * e + 1]);
-        *(i32x4*)((bf16_t*)p.y + pix * p.y_ld + co) = o;
-      }
-    }
-  }
-}
-
-// DVIE_1X1_STREAM: 0 = the tiled single-K-step kernels (A/B runs), 2 / 4 = 32-channel blocks
-// per wave item (default 2); read per launch
-static int stream_env() {
-  const char* e = getenv("DVIE_1X1_STREAM");
-  return e && *e ? atoi(e) : 2;
-}
-
-template <int TMC>
-static void launch_1x1s(const dvie_conv_desc& p, hipStream_t s) {
-  const long long npix = (long long)p.n * p.oh * p.ow;
-  const int n_cg = (p.cout + 32 * TMC - 1) / (32 * TMC);
-  const long long n_items = ((npix + 31) / 32) * n_cg;
-  const long long want = (n_items + 3) / 4;
-  const int grid = (int)(want < 1024 ? want : 1024);  // 4 workgroups (16 waves) per CU
-  const int epi = (p.res ? 1 : 0) | (p.beta ? 2 : 0) | (p.dact ? 4 : 0);
-  switch (epi) {
-#define DVIE_1X1S_CASE(V)                                                                              \
-  case V:                                                                                              \
-    hipLaunchKernelGGL((conv1x1s_kernel<TMC, V>), dim3(grid), dim3(256), 0, s, p, n_cg, n_items); \
-    break;
-    DVIE_1X1S_CASE(0) DVIE_1X1S_CASE(1) DVIE_1X1S_CASE(2) DVIE_1X1S_CASE(3) DVIE_1X1S_CASE(4) DVIE_1X1S_CASE(5)
-    DVIE_1X1S_CASE(6) DVIE_1X1S_CASE(7)
-#undef DVIE_1X1S_CASE
-  }
-}
-
 // Returns true when the 1x1 GEMM kernel took the launch.
 bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (p.dtype != DVIE_BF16 || p.th != 1 || p.tw != 1) return false;
@@ -773,14 +628,7 @@ bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (cfg >= 0 && cfg < 100) return false;  // tuning override forces the halo / per-tap kernels
   const int cout = p.cout;
   const bool one = p.c <= 64;  // a single K-step: one stage, several workgroups per CU
-  const bool ident = p.osy == 1 && p.osx == 1 && p.ory == 0 && p.orx == 0 && p.yh == p.oh && p.yw == p.ow;
-  if (one && ident && !p.out_f32 && cout <= 256 && cfg < 0) {
-    const int st = stream_env();
-    if (st == 2 || st == 4) {
-      st == 4 ? launch_1x1s<4>(p, s) : launch_1x1s<2>(p, s);
-      return true;
-    }
-  }
+
   // wide layers: 2-D wave grid (116; 448->448 heads 724 -> 662 us, 64->256 166 -> 155 us
   // at 8x256x512, tools/conv_tune.py)
   // (DVIE_CONV1X1_WIDE overrides the wide-layer choice alone, for A/B runs of the whole step)

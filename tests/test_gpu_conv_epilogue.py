@@ -2,7 +2,7 @@
 residual / accumulate (beta) / activation / activation derivative, on the kernels the
 library picks by shape: weight-stationary 3x3 (c, cout <= 64, >= 65536 output pixels),
 the chunked halo kernel (128- and 64-channel output tiles), the dense-K kernel (c <= 24)
-and the 1x1 GEMM (tiled, persistent, and the streaming single-K-step kernel).  Ragged output sizes put lanes past the image edge in every tile row.
+and the 1x1 GEMM (tiled and persistent).  Ragged output sizes put lanes past the image edge in every tile row.
 
 Reference: bf16-rounded operands, conv in fp32 (torch CPU), the same epilogue order
 (acc + bias + res + y_old -> act -> dact(z)); tolerance 1e-2 relative to max |y| (bf16
@@ -27,8 +27,8 @@ SHAPES = [  # n, H, W, c, cout, k
     (2, 37, 77, 64, 256, 1),    # 1x1 single K-step, 64-pixel x 128-channel wave tiles: one operand prefetched
     (2, 37, 77, 64, 64, 1),     # 1x1 single K-step, every operand prefetched
     (2, 37, 77, 48, 128, 1),    # 1x1 single K-step, 48 input channels (zero-padded K)
-    (2, 37, 77, 32, 96, 1),     # 1x1 single K-step, streaming kernel: partial 64-channel item
-    (1, 33, 65, 64, 256, 1),    # 1x1 single K-step, streaming kernel: ragged last 32-pixel item
+    (2, 37, 77, 32, 96, 1),     # 1x1 single K-step, 32 input channels, partial 64-channel column tile
+    (1, 33, 65, 64, 256, 1),    # 1x1 single K-step, ragged pixel count
     (4, 128, 160, 128, 256, 1),  # 1x1 several K-steps, more tiles than resident workgroups: persistent
     (4, 128, 160, 256, 64, 1),   # the same, 64-channel tiles (3-stage ring)
     (3, 131, 177, 192, 96, 1),   # the same, ragged pixel count, partial 128-channel tile
