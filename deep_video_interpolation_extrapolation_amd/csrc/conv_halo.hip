@@ -214,6 +214,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   // (a job past the end still issues its pieces, with an empty buffer range: they land as
   // zeros in a buffer nobody reads, and every wave's vmcnt bookkeeping stays compile-time)
   auto halo_issue = [&](const JobInfo& J, int hb, int qa, int qb) {
+    if (epi_pre & 16) return;  // timing experiments only (DVIE_HALO_DBG): no halo streaming
     const int nrec = J.valid ? (int)(xbytes - (unsigned long long)J.k * 128) : 0;
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)J.k * 128), 0, nrec, 0x00020000);
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   };
   // weights of (job J, tap t) into weight buffer ab
   auto a_issue = [&](const JobInfo& J, int t, int ab) {
+    if (epi_pre & 8) return;  // timing experiments only (DVIE_HALO_DBG): no weight streaming
     const unsigned o = (unsigned)((long long)J.c0 * p.kpad + t * p.c + 64 * J.k) * 2u;
     const int nrec = J.valid ? (int)((unsigned)p.cout * (unsigned)p.kpad * 2u - o) : 0;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + o), 0, nrec, 0x00020000);
@@ -292,6 +294,8 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   };
 
   // ---- prologue: job 0 halo (+ job 1 for 1x1), weights of steps 0 and 1 ----
+  const int dbg = epi_pre & 24;
+  epi_pre &= ~24;
   {
     const JobInfo J0 = tile_job(tile0);
     halo_issue(J0, 0, 0, C::NHQ);
@@ -307,6 +311,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
     __syncthreads();
   }
 
+  epi_pre |= dbg;
   int sc = 0;  // global step counter (weight ring position)
   JobInfo J = tile_job(tile0);
   JobInfo J1 = next_job(J);
@@ -504,7 +509,8 @@ static const int halo_setprio = getenv("DVIE_SETPRIO") && *getenv("DVIE_SETPRIO"
 // DVIE_HALO_WAIT=0: every step waits for all loads issued before it (A/B runs); read per launch
 static int halo_wait_flag() {
   const char* e = getenv("DVIE_HALO_WAIT");
-  return e && *e == '0' ? 0 : 4;
+  const char* d = getenv("DVIE_HALO_DBG");  // timing experiments only: 8 = no weight, 16 = no halo streaming
+  return (e && *e == '0' ? 0 : 4) | (d && *d ? (atoi(d) & 24) : 0);
 }
 
 template <int TM, int WC, int WP, int TH, int TW>
