@@ -177,6 +177,31 @@ def warp_roofline(dev, n, H, W, reps=20):
     return res
 
 
+def mfma_probe(dev, blocks=2048, iters=16384, reps=5):
+    """Dense bf16 MFMA rate this box sustains under load (dvie_mfma_probe: 4-wave workgroups filling every CU,
+    back-to-back v_mfma_f32_32x32x16_bf16 on pseudo-random register operands, 32768 FLOP
+    each), timed with HIP events on the launch stream.  The chip lowers its clock under
+    random-data MFMA load (MI355X_MICROARCH.md), so this, not the 2.5 PF spec, is the ceiling
+    a conv kernel can reach on the same box; reported beside `frac` as `frac_of_mfma_loop`."""
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    lib = L.load()
+    out = torch.empty(blocks * 256, device=dev)
+    s = L.stream_ptr(dev)
+    for _ in range(10):  # ~0.3 s of load first, so the clock has settled
+        L.check(lib.dvie_mfma_probe(out.data_ptr(), blocks, iters, s), "mfma probe")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        L.check(lib.dvie_mfma_probe(out.data_ptr(), blocks, iters, s), "mfma probe")
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flop = blocks * 4 * 8 * iters * 32768.0
+    return {"tflops": round(flop / (ms * 1e-3) / 1e12, 1), "ms": round(ms, 3), "blocks": blocks, "iters": iters,
+            "finite": bool(torch.isfinite(out).all())}
+
+
 def clip_prep_roofline(dev, n, H, W, reps=20):
     """Device clip pipeline (data.DeviceClips / dvie_clip_prep; the reference's DataLoader
     worker, folder.py:207-247): n 3-frame clips from an HBM-resident uint8 store of
@@ -359,6 +384,10 @@ def main():
                 "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4),
                 # sum over launches of max(F/P_mfma, B/BW_hbm) over measured time
                 "per_op_roofline_time_frac": round(sum(r["roof_ms"] for r in conv) / ms, 4)}
+        mp = mfma_probe(dev) if a.precision == "bf16" else None
+        if mp:
+            roof["mfma_loop"] = mp
+            roof["frac_of_mfma_loop"] = round(tf / mp["tflops"], 4)
         wg = agg.get("conv_wgrad")
         if wg:  # weight gradients: algorithmic bytes (x, dy read once, dW written) vs PMC traffic
             roof["wgrad"] = {"launches_per_step": wg["n"] // max(1, a.profile_steps),

@@ -200,7 +200,7 @@ EXPORTS = [
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
-    "dvie_adam_dev",
+    "dvie_adam_dev", "dvie_mfma_probe",
 ]
 
 _lib = None
@@ -255,6 +255,8 @@ def load():
         lib.dvie_adamax_dev.argtypes = [vp, vp, vp, vp, i64, f64, f64, f64, f64, f64, vp, vp]
         lib.dvie_adam_dev.argtypes = [vp, vp, vp, vp, i64, f64, f64, f64, f64, f64, vp, vp]
         lib.dvie_step_inc.argtypes = [vp, vp]
+        lib.dvie_mfma_probe.argtypes = [vp, i32, i32, vp]
+        lib.dvie_mfma_probe.restype = i32
         for name in ("dvie_sn_fwd", "dvie_sn_bwd"):
             getattr(lib, name).argtypes = [vp, i32, vp, vp]
             getattr(lib, name).restype = i32

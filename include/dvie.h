@@ -332,6 +332,14 @@ int dvie_adamax_dev(float* p, const float* g, float* m, float* u, long long n, d
 int dvie_scale(float* p, long long n, float s, void* stream);
 
 /*
+ * Measurement only (bench.py): `blocks` workgroups of 4 waves, each wave issuing
+ * 8 * iters back-to-back v_mfma_f32_32x32x16_bf16 on pseudo-random operands in registers
+ * (32768 FLOP each); out[blocks * 256] receives per-lane sums.  Its rate is the dense bf16
+ * MFMA ceiling at the clock the chip holds under that load on this box.
+ */
+int dvie_mfma_probe(float* out, int blocks, int iters, void* stream);
+
+/*
  * BatchNorm2d over NHWC rows (rows = N*H*W pixels, c channels), fused with the following
  * activation (nets/FrameDisc.py:45-46, nets/VidDisc.py:45-50, nets/HRNet.py:726-789).
  * training = 1: batch statistics (biased variance for the normalisation; running_mean /
