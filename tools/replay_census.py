@@ -2,6 +2,7 @@
 
     python tools/replay_census.py run [replays]        (under rocprofv3 --kernel-trace)
     python tools/replay_census.py report <kernel_trace.csv>
+    python tools/replay_census.py aten [H W batch]     (no profiler: aten ops of one eager step)
 
 `run` builds the bench trainer (InterNet 256x512 bf16, batch 8), captures the step
 (runners/graph.py) and replays it, each replay preceded by a marker kernel
@@ -43,6 +44,54 @@ def run(replays):
     print("replays", replays)
 
 
+def aten(H=256, W=512, B=8):
+    """Every aten op one eager bench step dispatches (views and metadata ops excluded), with
+    the Python frame in this package that issued it: the PyTorch glue left around the
+    native plan launches."""
+    import traceback
+    import torch
+    from torch.utils._python_dispatch import TorchDispatchMode
+    sys.argv = [sys.argv[0]]
+    import bench
+    from deep_video_interpolation_extrapolation_amd.options import default_args
+    from deep_video_interpolation_extrapolation_amd.runners.InterTrainer import InterTrainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    args = default_args("INTER", syn_type="inter", interval=5, mode="xs2xs", vid_length=1, train_coarse=True,
+                        batch_size=B, input_h=H, input_w=W, precision="bf16", synthetic=B, num_workers=0,
+                        split="train")
+    torch.manual_seed(args.seed)
+    tr = InterTrainer(args)
+    data = bench.make_batch(B, H, W, dev, 0)
+    tr.step(data)
+    tr.step(data)
+    torch.cuda.synchronize()
+    skip = ("view", "_unsafe_view", "as_strided", "alias", "detach", "t.default", "expand", "slice", "select",
+            "unsqueeze", "squeeze", "permute", "transpose", "split", "unbind", "_to_copy", "lift_fresh",
+            "is_same_size", "empty", "_local_scalar_dense", "item")
+    seen = collections.Counter()
+    where = {}
+
+    class Log(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = str(func)
+            if not any(name.startswith("aten." + k) for k in skip):
+                fr = [f for f in traceback.extract_stack()
+                      if "deep_video_interpolation_extrapolation_amd" in f.filename]
+                loc = f"{os.path.basename(fr[-1].filename)}:{fr[-1].lineno}" if fr else "?"
+                shp = [tuple(a.shape) for a in args if isinstance(a, torch.Tensor)][:2]
+                seen[(name, loc)] += 1
+                where.setdefault((name, loc), shp)
+            return func(*args, **(kwargs or {}))
+
+    with Log():
+        tr.step(data)
+    torch.cuda.synchronize()
+    print(f"aten ops of one eager step at {B}x{H}x{W}: {sum(seen.values())}")
+    for (name, loc), n in seen.most_common():
+        print(f"    {n:4d}  {name:40s} {loc:28s} {where[(name, loc)]}")
+
+
 def family(name):
     n = re.sub(r"\(.*", "", name)
     n = re.sub(r"<.*", "", n).replace("void ", "")
@@ -73,5 +122,7 @@ def report(path):
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(int(sys.argv[2]) if len(sys.argv) > 2 else 3)
+    elif sys.argv[1] == "aten":
+        aten(*[int(v) for v in sys.argv[2:5]])
     else:
         report(sys.argv[2])
