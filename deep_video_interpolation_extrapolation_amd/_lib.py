@@ -103,8 +103,8 @@ class LossDesc(ctypes.Structure):
         ("a_sn", i64), ("a_sc", i64), ("a_sh", i64), ("a_sw", i64),
         ("b_sn", i64), ("b_sc", i64), ("b_sh", i64), ("b_sw", i64),
         ("kind", i32), ("bsz", i32), ("ch", i32), ("h", i32),
-        ("w", i32), ("beta", i32), ("dtype", i32), ("pad0", i32),
-        ("weight", f32), ("pad1", f32),
+        ("w", i32), ("beta", i32), ("dtype", i32), ("out_acc", i32),
+        ("weight", f32), ("out_scale", f32),
     ]
 
 
@@ -200,7 +200,7 @@ EXPORTS = [
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
-    "dvie_adam_dev", "dvie_mfma_probe",
+    "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32",
 ]
 
 _lib = None
@@ -257,6 +257,8 @@ def load():
         lib.dvie_step_inc.argtypes = [vp, vp]
         lib.dvie_mfma_probe.argtypes = [vp, i32, i32, vp]
         lib.dvie_mfma_probe.restype = i32
+        lib.dvie_sum_f32.argtypes = [vp, i32, vp, vp]
+        lib.dvie_sum_f32.restype = i32
         for name in ("dvie_sn_fwd", "dvie_sn_bwd"):
             getattr(lib, name).argtypes = [vp, i32, vp, vp]
             getattr(lib, name).restype = i32

@@ -270,7 +270,10 @@ __global__ __launch_bounds__(256) void ew_kernel(const dvie_ew_desc p, int cq) {
       for (int k = 0; k < VW; ++k) {
         const int ch = c + k;
         if (ch < p.ext_c) {
-          float t = p.ext[(long long)n * p.sn + (long long)ch * p.sc + (long long)y * p.sh + (long long)x * p.sw];
+          const bool second = p.src1 != nullptr && ch >= p.sh1;
+          const float* e = second ? (const float*)p.src1 : p.ext;
+          const int cc = second ? ch - p.sh1 : ch;
+          float t = e[(long long)n * p.sn + (long long)cc * p.sc + (long long)y * p.sh + (long long)x * p.sw];
           if (p.mean) t = (t - p.mean[ch]) / p.std[ch];
           v[k] = t;
         }

@@ -422,14 +422,27 @@ __global__ __launch_bounds__(256) void ssim_bwd_kernel(const dvie_loss_desc p) {
   }
 }
 
+// out[j] (+)= vscale * (sum of partials * mul + add)
 __global__ __launch_bounds__(RB) void finalize_kernel(const double* part, int nb, int nout, float* out, double mul,
-                                                      double add) {
+                                                      double add, float vscale, int acc) {
   __shared__ double sh[RB / 64];
   for (int j = 0; j < nout; ++j) {
     double s = 0.0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[(long long)j * nb + i];
     const double t = block_sum(s, sh);
-    if (threadIdx.x == 0) out[j] = (float)(t * mul + add);
+    if (threadIdx.x == 0) {
+      const float v = vscale * (float)(t * mul + add);
+      out[j] = acc ? out[j] + v : v;
+    }
+  }
+}
+
+// one workgroup: out[0] = x[0] + x[1] + ... in index order (lane 0 walks the terms)
+__global__ __launch_bounds__(64) void sum_f32_kernel(const float* x, int n, float* out) {
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += x[i];
+    out[0] = s;
   }
 }
 
@@ -512,6 +525,8 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
     DVIE_CHECK_ARG(d->grad == nullptr, "loss: kind %d is a metric (no gradient)", d->kind);
   hipStream_t s = (hipStream_t)stream;
   const LossPlan lp = plan_loss(*d);
+  const float vs = d->out_scale != 0.f ? d->out_scale : 1.f;
+  const int acc = d->out_acc;
   const double px = (double)d->bsz * d->h * d->w;
   const double tot = px * d->ch;
   switch (d->kind) {
@@ -519,21 +534,21 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
     case DVIE_LOSS_GDL:
       hipLaunchKernelGGL(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, 0);
       hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
-                         d->kind == DVIE_LOSS_L1 ? 1.0 / tot : 1.0, 0.0);
+                         d->kind == DVIE_LOSS_L1 ? 1.0 / tot : 1.0, 0.0, vs, acc);
       break;
     case DVIE_LOSS_MSE:
       hipLaunchKernelGGL(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, lp.per_sample);
       hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.per_sample, d->bsz, d->out,
-                         1.0 / ((double)d->ch * d->h * d->w), 0.0);
+                         1.0 / ((double)d->ch * d->h * d->w), 0.0, vs, acc);
       break;
     case DVIE_LOSS_CE:
       hipLaunchKernelGGL(ce_kernel, lp.grid, dim3(RB), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0, vs, acc);
       break;
     case DVIE_LOSS_SSIM:
       hipLaunchKernelGGL(ssim_fwd_kernel, lp.grid, dim3(256), 0, s, *d);
       hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, -1.0 / tot,
-                         1.0);
+                         1.0, vs, acc);
       if (d->grad) hipLaunchKernelGGL(ssim_bwd_kernel, lp.grid, dim3(256), 0, s, *d);
       break;
     case DVIE_LOSS_L1NHWC:
@@ -541,7 +556,7 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
         hipLaunchKernelGGL(l1nhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d);
       else
         hipLaunchKernelGGL(l1nhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / tot, 0.0);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / tot, 0.0, vs, acc);
       break;
     case DVIE_LOSS_COSNHWC:
       if (d->dtype == DVIE_BF16)
@@ -549,16 +564,22 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
       else
         hipLaunchKernelGGL(cosnhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
       hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
-                         (double)d->weight / px, 0.0);
+                         (double)d->weight / px, 0.0, vs, acc);
       break;
     case DVIE_LOSS_IOU:
     case DVIE_LOSS_ARGMAX_IOU:
       hipLaunchKernelGGL(iou_kernel, lp.grid, dim3(RB), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0);
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0, vs, acc);
       break;
     default:
       DVIE_CHECK_ARG(false, "loss: unknown kind %d", d->kind);
   }
+  DVIE_RETURN_LAUNCH();
+}
+
+int dvie_sum_f32(const float* x, int n, float* out, void* stream) {
+  DVIE_CHECK_ARG(x && out && n > 0, "sum_f32: args");
+  hipLaunchKernelGGL(sum_f32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, x, n, out);
   DVIE_RETURN_LAUNCH();
 }
 

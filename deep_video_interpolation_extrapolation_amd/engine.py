@@ -541,6 +541,7 @@ class Plan:
         self._alloc()
         self.fwd = []
         self.bwd = []
+        self._l1_fwd = []  # (forward list index, level) of the VGG feature-L1 loss ops
         self.ext_in = {}  # key -> list of (op index, InputOp) for patching
         self.ext_out = {}
         self.ext_grad = {}  # key -> list of bwd op indices (TONCHW)
@@ -841,6 +842,7 @@ class Plan:
                 self.keep.append(part)
                 d.partial = part.data_ptr()
                 d.out = self.l1_out.data_ptr() + 4 * op.idx
+                self._l1_fwd.append((len(self.fwd), op.idx))
                 self.fwd.append(o)
             else:
                 raise TypeError(op)
@@ -1077,8 +1079,10 @@ class Plan:
                 scale = op.weight / numel
 
                 def em(beta, res, res_ld, dact, z, z_ld, a=a, ap=ap, bp=bp, ld=ld, gp=gp, scale=scale):
-                    return [self.ew_desc(L.EW_L1SIGN, nb, a.H, a.W, a.c, gp, ld, [(ap, ld, a.H, a.W), (bp, ld, a.H, a.W)],
-                                         res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta, scale=scale)]
+                    o = self.ew_desc(L.EW_L1SIGN, nb, a.H, a.W, a.c, gp, ld, [(ap, ld, a.H, a.W), (bp, ld, a.H, a.W)],
+                                     res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta, scale=scale)
+                    o.l1_seed = scale  # set_l1_loss rescales the seeds of the backward
+                    return [o]
 
                 self._contrib(a, em)
                 continue
@@ -1413,6 +1417,32 @@ class Plan:
             sn, sc, sh, sw = t.stride()
             d.ext = t.data_ptr() + 4 * op.ext_c0 * sc
             d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+            d.src1, d.sh1 = None, 0
+
+    def set_input_parts(self, key, parts):
+        """set_input for an input given as consecutive channel blocks (the frames of a clip
+        as separate NCHW fp32 tensors of equal shape and strides) instead of one concatenated
+        tensor: each input op reads its channels in place; an op whose channels straddle two
+        blocks reads the second through the EW_NCHW split (src1 / sh1)."""
+        starts = [0]
+        for t in parts:
+            assert t.dtype == torch.float32 and t.device.type == self.device.type
+            assert t.stride() == parts[0].stride() and t.shape[0] == parts[0].shape[0], (key, t.shape, t.stride())
+            starts.append(starts[-1] + t.shape[1])
+        for idx, op in self.ext_in[key]:
+            d = self.fwd_arr[idx + self.fwd_off].u.ew
+            j = max(i for i in range(len(parts)) if starts[i] <= op.ext_c0)
+            t = parts[j]
+            assert t.shape[0] == self._part(op.part)[1] and t.shape[2:] == (op.out.H, op.out.W), (key, tuple(t.shape))
+            sn, sc, sh, sw = t.stride()
+            d.ext = t.data_ptr() + 4 * (op.ext_c0 - starts[j]) * sc
+            d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+            end = op.ext_c0 + op.ext_c
+            if end > starts[j + 1]:  # the op's channels continue in the next block
+                assert j + 1 < len(parts) and end <= starts[j + 2], (key, op.ext_c0, op.ext_c, starts)
+                d.src1, d.sh1 = parts[j + 1].data_ptr(), starts[j + 1] - op.ext_c0
+            else:
+                d.src1, d.sh1 = None, 0
 
     def set_output(self, name, t):
         for idx, region in self.ext_out[name]:
@@ -1456,6 +1486,25 @@ class Plan:
         sn, sc, sh, sw = t.stride()
         d.ext = t.data_ptr()
         d.sn, d.sc, d.sh, d.sw = sn, sc, sh, sw
+
+    def set_l1_loss(self, out=None, value_scale=1.0, grad_scale=1.0):
+        """Where the VGG feature-L1 loss ops put their values, and the gradient scale.
+        out None: level k's mean into l1_out[k] (the autograd path, VGGLoss); a 1-element
+        fp32 tensor: value_scale * (mean over levels of the level means) into out[0] (the
+        levels add into it in order, no PyTorch reduction).  grad_scale multiplies the
+        backward seeds, so the input gradient is grad_scale * d(loss)/d(pred)."""
+        nl = max(1, len(self._l1_fwd))
+        for k, (idx, lev) in enumerate(self._l1_fwd):
+            d = self.fwd_arr[idx + self.fwd_off].u.loss
+            if out is None:
+                d.out, d.out_acc, d.out_scale = self.l1_out.data_ptr() + 4 * lev, 0, 1.0
+            else:
+                d.out, d.out_acc, d.out_scale = out.data_ptr(), int(k > 0), value_scale / nl
+        if self.bwd_arr is not None:
+            if not hasattr(self, "_l1_bwd"):
+                self._l1_bwd = [(i, o.l1_seed) for i, o in enumerate(self.bwd) if hasattr(o, "l1_seed")]
+            for i, base in self._l1_bwd:
+                self.bwd_arr[i].u.ew.scale = base * grad_scale
 
     def set_input_grad(self, key, t, accumulate=False):
         for idx, op in self.ext_grad[key]:

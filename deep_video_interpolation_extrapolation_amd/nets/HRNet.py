@@ -496,8 +496,15 @@ class HRNet(FlatParams, nn.Module):
         L.require_gpu(x)
         xgrad = bool(train) and bool(getattr(self, "_in_needs", (False,))[0])
         plan = self._pool.acquire((n, H, W, self.dtype, bool(train), x.device, xgrad, bool(self.export_stem)))
-        plan.set_input("x", x)
-        plan.set_input("seg", seg)
+        xs, ss = getattr(self, "_parts", (None, None))
+        if xs is not None:
+            plan.set_input_parts("x", xs)
+        else:
+            plan.set_input("x", x)
+        if ss is not None:
+            plan.set_input_parts("seg", ss)
+        else:
+            plan.set_input("seg", seg)
         if self.export_stem:
             F = self.n_frames
             stem = torch.empty((n, 7 * F, H, W), dtype=torch.float32, device=x.device)
@@ -574,10 +581,27 @@ class HRNet(FlatParams, nn.Module):
         return [gx, None] + ([gv] if len(inputs) > 2 else [])
 
     def forward_split(self, x, seg):
-        """x: (B, 3F, H, W) frames in [-1, 1]; seg: (B, 20F, H, W) one-hot segmentations."""
-        x = x.float()
-        seg = seg.float()
-        return PlanFunction.apply(self, 2, x, seg, *self._flat_params)
+        """x: (B, 3F, H, W) frames in [-1, 1]; seg: (B, 20F, H, W) one-hot segmentations.
+        Either may also be a list of the F per-frame tensors ((B, 3, H, W) / (B, 20, H, W),
+        fp32, equal strides): the plan's input ops then read them in place, with no
+        concatenation (frames that need a gradient are concatenated)."""
+        xs = list(x) if isinstance(x, (list, tuple)) else None
+        ss = list(seg) if isinstance(seg, (list, tuple)) else None
+        def in_place(ts, grad_ok=False):
+            return (all(t.dtype == torch.float32 and t.stride() == ts[0].stride() and t.shape == ts[0].shape
+                        for t in ts) and (grad_ok or not any(t.requires_grad for t in ts)))
+
+        if xs is not None and not in_place(xs):
+            x, xs = torch.cat([t.float() for t in xs], 1), None
+        if ss is not None and not in_place(ss, grad_ok=True):
+            seg, ss = torch.cat([t.float() for t in ss], 1), None
+        x = xs[0] if xs is not None else x.float()  # stands in for the frames (shape, device)
+        seg = ss[0] if ss is not None else seg.float()
+        self._parts = (xs, ss)
+        try:
+            return PlanFunction.apply(self, 2, x, seg, *self._flat_params)
+        finally:
+            self._parts = (None, None)
 
     def forward(self, input):
         F = self.n_frames

@@ -141,6 +141,27 @@ class my_vgg(nn.Module):
         plan.run_backward()
         return [gp * go, None]
 
+    def perceptual_l1_into(self, pred, gt, normalize, out, value_scale, grad, grad_scale, accumulate):
+        """Explicit-gradient form of perceptual_l1 (losses.LossTape): one plan forward over
+        [pred | gt] writes value_scale * loss into out[0] (the five levels add into it);
+        the plan backward, its seeds scaled by grad_scale, writes (accumulate=False) or adds
+        grad_scale * d(loss)/d(pred) into grad (NCHW fp32).  No autograd node."""
+        n, _, H, W = pred.shape
+        L.require_gpu(pred)
+        plan = self._pool.acquire((n, H, W, self.dtype, bool(normalize), True, pred.device))
+        plan.busy = True
+        try:
+            plan.set_input("pred", pred)
+            plan.set_input("gt", gt)
+            plan.set_l1_loss(out, value_scale, grad_scale)
+            plan.run_forward()
+            plan.set_input_grad("pred", grad, accumulate=accumulate)
+            plan.run_backward()
+        finally:
+            plan.set_l1_loss(None)
+            plan.busy = False
+        self.last_plan = plan
+
     def perceptual_l1(self, pred, gt, normalize):
         self._normalize = bool(normalize)
         return PlanFunction.apply(self, 2, pred.float(), gt.float().detach())

@@ -29,6 +29,7 @@ import torch
 
 from .. import _lib as L
 from ..data import batch_to
+from ..losses import make_tape
 from . import comm
 from .InterTrainer import InterTrainer
 
@@ -68,7 +69,7 @@ class ExtraTrainer(InterTrainer):
         # after the last backward (see GradSync.set_overlap)
         self.model.set_overlap(nps == 1 and not getattr(self, "no_overlap", False))
         xs2xs = a.mode == "xs2xs"
-        loss_dict = OrderedDict()
+        tape = make_tape(self.device, self.W)
         last_rgb = torch.cat([data["frame1"], data["frame2"]], dim=1)
         last_seg = torch.cat([data["seg1"], data["seg2"]], dim=1) if xs2xs else None
         for ii in range(nps):
@@ -84,28 +85,24 @@ class ExtraTrainer(InterTrainer):
             coarse_img, coarse_seg = out[0], out[1]
             for j in range(npo):
                 prefix = "step_{}_frame_{}_coarse".format(ii + 1, j + 1)
-                loss_dict.update(self.RGBLoss(coarse_img[:, 3 * j:3 * j + 3], gt_x[:, 3 * j:3 * j + 3], False,
-                                              prefix=prefix))
+                tape.rgb(self.RGBLoss, coarse_img[:, 3 * j:3 * j + 3], gt_x[:, 3 * j:3 * j + 3], False, prefix=prefix)
                 if xs2xs:
-                    loss_dict[prefix + "_ce_loss"] = a.ce_weight * self.SegLoss(
-                        coarse_seg[:, 20 * j:20 * j + 20], gt_seg[:, 20 * j:20 * j + 20])
+                    tape.loss(prefix + "_ce_loss", L.LOSS_CE, coarse_seg[:, 20 * j:20 * j + 20],
+                              gt_seg[:, 20 * j:20 * j + 20], a.ce_weight)
             if self.refine:
-                self._refine_losses(loss_dict, out, gt_x, "step_{}_frame_1_".format(ii + 1))
+                self._refine_losses(tape, out, gt_x, "step_{}_frame_1_".format(ii + 1))
             if nps == 1:
                 break
             last_rgb = torch.cat([x[:, -3:], coarse_img], dim=1)
             if xs2xs:
                 last_seg = torch.cat([seg[:, -20:], onehot_argmax(coarse_seg)], dim=1)
-        loss = 0
-        for v in loss_dict.values():
-            loss = loss + torch.mean(v)
-        loss_dict["loss_all"] = loss
+        loss_dict = tape.loss_dict()
         for o in self._opts():
             o.zero_grad(set_to_none=True)
-        (loss / self.W).backward()  # reference `sync` divides loss_all by W in place (l.317, 760-765)
+        tape.backward()  # reference `sync` divides loss_all by W in place (l.317, 760-765)
         return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
 
-    def _refine_losses(self, loss_dict, out, gt_x, prefix):
+    def _refine_losses(self, tape, out, gt_x, prefix):
         """Second-stage losses of the two-stage extrapolation nets (ExtraRefineNet /
         ExtraStage3Net), the structure of the reference InterTrainer's (l.415-425): per scale
         the refine RGBLoss and (--stage3) the stage-3 RGBLoss against the target frame
@@ -114,9 +111,9 @@ class ExtraTrainer(InterTrainer):
         for i in range(a.n_scales):
             tag = str(1 / (2 ** (a.n_scales - i - 1)))
             gts = self._scale_gt(gt_x, i)
-            loss_dict.update(self.refine_RGBLoss(out[2][i], gts, False, prefix=prefix + "refine_" + tag))
+            tape.rgb(self.refine_RGBLoss, out[2][i], gts, False, prefix=prefix + "refine_" + tag)
             if self.stage3:
-                loss_dict.update(self.refine_RGBLoss(out[3][i], gts, False, prefix=prefix + "stage3_" + tag))
+                tape.rgb(self.refine_RGBLoss, out[3][i], gts, False, prefix=prefix + "stage3_" + tag)
 
     def validate(self):
         """Reference l.421-583: per (step, frame) L1 / PSNR / SSIM / IoU / VGG-cos."""

@@ -16,8 +16,9 @@ from collections import OrderedDict
 
 import torch
 
+from .. import _lib as L
 from ..data import batch_to
-from ..losses import GANScalarLoss, KLDLoss
+from ..losses import GANScalarLoss, KLDLoss, make_tape
 from ..optim import Adam, Adamax
 from . import comm
 from .InterTrainer import InterTrainer
@@ -79,26 +80,23 @@ class InterGANTrainer(InterTrainer):
         self.global_step += 1
         on = 1.0 if self.global_step > GAN_TRAIN_STEP else 0.0
         prefix = "coarse"
-        loss_dict = OrderedDict()
-        loss_dict.update(self.RGBLoss(self.normalize(coarse_img), self.normalize(gt_x), False, prefix=prefix))
-        loss_dict[prefix + "_ce_loss"] = a.ce_weight * self.SegLoss(coarse_seg, gt_seg)
+        tape = make_tape(self.device, self.W)
+        tape.rgb(self.RGBLoss, self.normalize(coarse_img), self.normalize(gt_x), False, prefix=prefix)
+        tape.loss(prefix + "_ce_loss", L.LOSS_CE, coarse_seg, gt_seg, a.ce_weight)
         if getattr(a, "vae", False) and mu is not None:
-            loss_dict[prefix + "_kld_loss"] = self.KLDLoss(mu, logvar)
+            tape.scalar(prefix + "_kld_loss", self.KLDLoss(mu, logvar))
         if getattr(a, "frame_disc", False):
-            loss_dict["coarse_frame_loss"] = self.FrameDisc_GLoss(G_fake_frame, True) * on
-            loss_dict["disc_frame_real_loss"] = self.FrameDisc_DLoss(D_real_frame, True) * on
-            loss_dict["disc_frame_fake_loss"] = self.FrameDisc_DLoss(D_fake_frame, False) * on
+            tape.scalar("coarse_frame_loss", self.FrameDisc_GLoss(G_fake_frame, True) * on)
+            tape.scalar("disc_frame_real_loss", self.FrameDisc_DLoss(D_real_frame, True) * on)
+            tape.scalar("disc_frame_fake_loss", self.FrameDisc_DLoss(D_fake_frame, False) * on)
         if getattr(a, "video_disc", False):
-            loss_dict["coarse_video_loss"] = self.VideoDisc_GLoss(G_fake_video, True) * on
-            loss_dict["disc_video_real_loss"] = self.VideoDisc_DLoss(D_real_video, True) * on
-            loss_dict["disc_video_fake_loss"] = self.VideoDisc_DLoss(D_fake_video, False) * on
-        loss = 0
-        for v in loss_dict.values():
-            loss = loss + torch.mean(v)
-        loss_dict["loss_all"] = loss
+            tape.scalar("coarse_video_loss", self.VideoDisc_GLoss(G_fake_video, True) * on)
+            tape.scalar("disc_video_real_loss", self.VideoDisc_DLoss(D_real_video, True) * on)
+            tape.scalar("disc_video_fake_loss", self.VideoDisc_DLoss(D_fake_video, False) * on)
+        loss_dict = tape.loss_dict()
         for o in self._gan_opts().values():
             o.zero_grad(set_to_none=True)
-        (loss / self.W).backward()  # reference `sync` divides loss_all by W in place (l.442, 902-907)
+        tape.backward()  # reference `sync` divides loss_all by W in place (l.442, 902-907)
         return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
 
     def apply_gradients(self, reduce=True):

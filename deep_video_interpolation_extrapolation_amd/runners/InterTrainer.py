@@ -23,7 +23,8 @@ import torch.distributed as dist
 
 from .. import nets
 from ..data import DeviceClipLoader, batch_to, get_dataset, load_clip_store
-from ..losses import IoU, L1Loss, PSNR, RGBLoss, SegCrossEntropy, SSIM, VGGCosineLoss
+from .. import _lib as L
+from ..losses import IoU, L1Loss, make_tape, PSNR, RGBLoss, SegCrossEntropy, SSIM, VGGCosineLoss
 from ..optim import Adamax
 from ..utils.net_utils import AverageMeter
 from . import comm
@@ -121,8 +122,14 @@ class InterTrainer:
     def get_input(self, data):
         gt_x = data["frame2"]
         gt_seg = data["seg2"] if self.args.mode == "xs2xs" else None
-        x = torch.cat([data["frame1"], data["frame3"]], dim=1)
-        seg = torch.cat([data["seg1"], data["seg3"]], dim=1) if self.args.mode == "xs2xs" else None
+        if getattr(self.args, "model", "InterNet") == "InterNet":
+            # the reference's torch.cat (l.373-374), left to the HRNet plan: its input ops read
+            # the frames and segmentations in place (HRNet.forward_split)
+            x = [data["frame1"], data["frame3"]]
+            seg = [data["seg1"], data["seg3"]] if self.args.mode == "xs2xs" else None
+        else:
+            x = torch.cat([data["frame1"], data["frame3"]], dim=1)
+            seg = torch.cat([data["seg1"], data["seg3"]], dim=1) if self.args.mode == "xs2xs" else None
         return x, seg, gt_x, gt_seg
 
     def _scale_gt(self, gt_x, i):
@@ -162,30 +169,25 @@ class InterTrainer:
         a = self.args
         data = batch_to(data, self.device)
         x, seg, gt_x, gt_seg = self.get_input(data)
-        loss_dict = OrderedDict()
         out = self.model(x, seg=seg)
-        coarse_img, coarse_seg = out[0], out[1]
-        prefix = "coarse"
-        loss_dict.update(self.RGBLoss(coarse_img, gt_x, False, prefix=prefix))
+        # reference l.401-431: RGBLoss + 30 CE (+ per-scale refine / stage-3 RGBLoss),
+        # loss_all = their sum, loss_all / W backward (losses.LossTape: the kernels write the
+        # weighted values and the gradients; no PyTorch kernel in between)
+        tape = make_tape(self.device, self.W)
+        tape.rgb(self.RGBLoss, out[0], gt_x, False, prefix="coarse")
         if a.mode == "xs2xs":
-            loss_dict[prefix + "_ce_loss"] = a.ce_weight * self.SegLoss(coarse_seg, gt_seg)
+            tape.loss("coarse_ce_loss", L.LOSS_CE, out[1], gt_seg, a.ce_weight)
         if self.refine:  # reference l.415-425 (per scale: refine, then stage 3)
-            refine_imgs = out[2]
-            stage3_imgs = out[3] if self.stage3 else None
             for i in range(a.n_scales):
                 tag = str(1 / (2 ** (a.n_scales - i - 1)))
                 gts = self._scale_gt(gt_x, i)
-                loss_dict.update(self.refine_RGBLoss(refine_imgs[i], gts, False, prefix="refine_" + tag))
+                tape.rgb(self.refine_RGBLoss, out[2][i], gts, False, prefix="refine_" + tag)
                 if self.stage3:
-                    loss_dict.update(self.refine_RGBLoss(stage3_imgs[i], gts, False, prefix="stage3_" + tag))
-        loss = 0
-        for v in loss_dict.values():
-            loss = loss + torch.mean(v)
-        loss_dict["loss_all"] = loss
+                    tape.rgb(self.refine_RGBLoss, out[3][i], gts, False, prefix="stage3_" + tag)
+        loss_dict = tape.loss_dict()
         for o in self._opts():
             o.zero_grad(set_to_none=True)
-        # reference `sync` divides loss_all by W in place before backward (l.431, 859-864)
-        (loss / self.W).backward()
+        tape.backward()
         return OrderedDict((k, v.detach()) for k, v in loss_dict.items())
 
     def _opts(self):

@@ -183,7 +183,10 @@ int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, voi
  *  DVIE_EW_L1SIGN y = scale * sign(src_0 - src_1) (VGG feature-L1 gradient, losses.py:178-179)
  *  DVIE_EW_NCHW   y = ext (fp32, arbitrary NCHW strides sn,sc,sh,sw; channels >= ext_c
  *                 read as zero), optionally (ext - mean[c]) / std[c]
- *                 (preprocess_norm, utils/net_utils.py:11-23).
+ *                 (preprocess_norm, utils/net_utils.py:11-23).  With src1 set, channels
+ *                 [sh1, ext_c) come from the fp32 tensor src1 (channel c - sh1, same
+ *                 strides): two frames read in place instead of torch.cat
+ *                 (runners/InterTrainer.py:373-374 of the reference).
  *  DVIE_EW_TONCHW ext (+)= channels [0, ext_c) of src_0 as fp32 with NCHW strides,
  *                 divided by std[c] when std is set (adjoint of the normalisation);
  *                 beta selects accumulate; the NHWC epilogue is not applied.
@@ -263,6 +266,13 @@ int dvie_ew(const dvie_ew_desc* d, void* stream);
 #define DVIE_LOSS_IOU 7
 #define DVIE_LOSS_ARGMAX_IOU 8
 
+/*
+ * grad (L1, GDL, SSIM, CE): d(weight * loss)/d(a), NCHW-contiguous fp32; beta = 1 adds it
+ * to what grad holds (several losses of one prediction write one gradient buffer).
+ * out: the loss value times out_scale (0 is read as 1, so zero-initialised descriptors
+ * report the plain value); out_acc = 1 adds it to *out instead of storing it (the five
+ * VGG feature levels into one scalar).  weight scales the gradient only (COSNHWC: the value).
+ */
 typedef struct dvie_loss_desc {
   const void* a;
   const void* b;
@@ -273,11 +283,16 @@ typedef struct dvie_loss_desc {
   long long a_sn, a_sc, a_sh, a_sw;
   long long b_sn, b_sc, b_sh, b_sw;
   int kind, bsz, ch, h;
-  int w, beta, dtype, pad0;
-  float weight, pad1;
+  int w, beta, dtype, out_acc;
+  float weight, out_scale;
 } dvie_loss_desc;
 
 int dvie_loss(const dvie_loss_desc* d, void* stream);
+
+/* out[0] = sum of x[0 .. n-1] in index order, one workgroup (the training step's loss_all
+ * from its weighted terms; replaces the Python sum at runners/InterTrainer.py:426-430 of
+ * the reference) */
+int dvie_sum_f32(const float* x, int n, float* out, void* stream);
 size_t dvie_loss_partial_count(const dvie_loss_desc* d);
 size_t dvie_loss_ws_floats(const dvie_loss_desc* d);
 

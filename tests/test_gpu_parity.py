@@ -216,6 +216,33 @@ def test_hrnet_forward_fp32_parity(dev, monkeypatch):
     assert float((s.cpu() - sr).abs().max()) < 1e-3
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_hrnet_frame_parts_match_concatenated(dev, monkeypatch, prec):
+    """HRNet.forward_split with the frames and segmentations as per-frame tensors (the plan's
+    input ops read them in place; the two-frame rgb op through the EW_NCHW src1 split) is
+    bit-identical to the concatenated input, for separate tensors and for channel views of
+    one tensor, and its backward gives the same parameter gradients."""
+    m = _hrnet(dev, prec, monkeypatch)
+    x, seg = inputs.hrnet_input(2, 32, 64)
+    x, seg = x.to(dev), seg.to(dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    w1, w2 = torch.randn((2, 3, 32, 64), generator=g, device=dev), torch.randn((2, 20, 32, 64), generator=g, device=dev)
+
+    def run(xi, si):
+        for p in m.parameters():
+            p.grad = None
+        rgb, s = m(xi, si)
+        ((rgb * w1).sum() + (s * w2).sum()).backward()
+        return rgb.detach().clone(), s.detach().clone(), [p.grad.clone() for p in m.parameters() if p.grad is not None]
+
+    ref = run(x, seg)
+    sep = run([x[:, :3].contiguous(), x[:, 3:].contiguous()], [seg[:, :20].contiguous(), seg[:, 20:].contiguous()])
+    views = run([x[:, :3], x[:, 3:]], [seg[:, :20], seg[:, 20:]])
+    for got in (sep, views):
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+        assert len(got[2]) == len(ref[2]) and all(torch.equal(a, b) for a, b in zip(got[2], ref[2]))
+
+
 def test_hrnet_backward_fp32_parity(dev, monkeypatch):
     """Parameter gradients vs an fp64 oracle's autograd on the same activation branches.
 
