@@ -52,7 +52,7 @@ class WgradDesc(ctypes.Structure):
         ("ih", i32), ("iw", i32), ("c", i32), ("sy", i32),
         ("sx", i32), ("th", i32), ("tw", i32), ("dy0", i32),
         ("dx0", i32), ("ddy", i32), ("ddx", i32), ("splits", i32),
-        ("dtype", i32), ("pad0", i32),
+        ("dtype", i32), ("pad0", i32), ("bws", vp),
     ]
 
 
@@ -200,7 +200,7 @@ EXPORTS = [
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
-    "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32",
+    "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs",
 ]
 
 _lib = None
@@ -259,6 +259,8 @@ def load():
         lib.dvie_mfma_probe.restype = i32
         lib.dvie_sum_f32.argtypes = [vp, i32, vp, vp]
         lib.dvie_sum_f32.restype = i32
+        lib.dvie_wgrad_bias_slabs.argtypes = [vp]
+        lib.dvie_wgrad_bias_slabs.restype = i32
         for name in ("dvie_sn_fwd", "dvie_sn_bwd"):
             getattr(lib, name).argtypes = [vp, i32, vp, vp]
             getattr(lib, name).restype = i32

@@ -383,6 +383,7 @@ using namespace dvie;
 namespace dvie {
 int wgrad_halo_splits(const dvie_wgrad_desc& p);  // wgrad_halo.hip
 int wgrad_halo_slabs(const dvie_wgrad_desc& p);
+int wgrad_halo_bias_slabs(const dvie_wgrad_desc& p);
 bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s);
 }  // namespace dvie
 
@@ -391,6 +392,35 @@ extern "C" {
 int dvie_wgrad_splits_hint(const dvie_wgrad_desc* d) { return d ? wgrad_halo_splits(*d) : 0; }
 
 int dvie_wgrad_slabs(const dvie_wgrad_desc* d) { return d ? wgrad_halo_slabs(*d) : 0; }
+
+// bias column sums as a pass of their own, for launches the halo kernels do not take
+static int colsum_bias_splits(const dvie_wgrad_desc& d) {
+  const long long npix = (long long)d.n * d.oh * d.ow;
+  const long long s = npix / 512;  // >= 8 blocks per CU at full resolution
+  return (int)(s < 1 ? 1 : (s > 2048 ? 2048 : s));
+}
+
+static void launch_bias_colsum(const dvie_wgrad_desc& d, hipStream_t s) {
+  dvie_colsum_desc c{};
+  c.g = d.g;
+  c.ws = d.bws;
+  c.g_ld = d.g_ld;
+  c.rows = (long long)d.n * d.oh * d.ow;
+  c.c = d.cout;
+  c.splits = colsum_bias_splits(d);
+  c.dtype = d.dtype;
+  const long long chunk = (c.rows + c.splits - 1) / c.splits;
+  if (d.dtype == DVIE_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(c.splits), dim3(256), 0, s, c, chunk);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(c.splits), dim3(256), 0, s, c, chunk);
+}
+
+int dvie_wgrad_bias_slabs(const dvie_wgrad_desc* d) {
+  if (!d) return 0;
+  const int h = wgrad_halo_bias_slabs(*d);
+  return h > 0 ? h : colsum_bias_splits(*d);
+}
 
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->g && d->x && d->ws, "wgrad: null pointer");
@@ -404,11 +434,13 @@ int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   chunk = (chunk + bkp - 1) / bkp * bkp;
   dim3 grid((unsigned)d->splits, (unsigned)(((d->cout + 63) / 64) * ((d->c + 63) / 64)), (unsigned)(d->th * d->tw));
   hipStream_t s = (hipStream_t)stream;
-  if (wgrad_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();
+  if (d->bws) DVIE_CHECK_ARG(d->cout % 4 == 0 && d->cout <= 4096 && d->g_ld % 4 == 0, "wgrad: bias partials (cout=%d)", d->cout);
+  if (wgrad_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();  // (bias sums fused when bws is set)
   if (d->dtype == DVIE_BF16)
     hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, *d, chunk);
   else
     hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, s, *d, chunk);
+  if (d->bws) launch_bias_colsum(*d, s);
   DVIE_RETURN_LAUNCH();
 }
 

@@ -36,6 +36,16 @@ __device__ __forceinline__ bf16x8 tr_pair(const char* p0, const char* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// sum of a fragment's 8 bf16 values in fp32 (bias column sums)
+__device__ __forceinline__ float sum8_bf16(const bf16x8 v) {
+  const i32x4 u = __builtin_bit_cast(i32x4, v);
+  float t = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    t += __uint_as_float(((uint32_t)u[e]) << 16) + __uint_as_float(((uint32_t)u[e]) & 0xffff0000u);
+  return t;
+}
+
 template <int TH, int TW, int PR, int TMO, int TMI>
 struct WgCfg {
   static constexpr int NT = TH * TW;
@@ -172,6 +182,12 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
     for (int e = 0; e < 16; ++e) acc[a][e] = 0.f;
 
   const int wco = (wave >> 1) & 1, wci = wave & 1, wrow = wave >> 2;
+  // bias gradient (p.bws): the ci-block-0 workgroups' wci = 0 waves sum the G fragments they
+  // already hold for the MFMAs (lane l: co = l % 32 of the fragment, 8 pixels)
+  const bool dob = p.bws != nullptr && kb == 0 && wci == 0;
+  float bsum[TMO];
+#pragma unroll
+  for (int j = 0; j < TMO; ++j) bsum[j] = 0.f;
   int g_off[TMO], x_off[4][TMI];
 #pragma unroll
   for (int j = 0; j < TMO; ++j) {
@@ -214,6 +230,10 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
         bf16x8 a[TMO];
 #pragma unroll
         for (int j = 0; j < TMO; ++j) a[j] = tr_pair(G + g_off[j] + gr * 128, G + g_off[j] + gr * 128 + 4 * 128);
+        if (dob) {
+#pragma unroll
+          for (int j = 0; j < TMO; ++j) bsum[j] += sum8_bf16(a[j]);
+        }
 #pragma unroll
         for (int ti = 0; ti < TH; ++ti) {
           const int slot = (T.y0 + py + ti) % C::R;  // ring slot of halo row py + ti (uniform)
@@ -242,6 +262,17 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
       issue_x(TN, 0, C::HR);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
+    }
+  }
+
+  // bias partials: lanes l and l + 32 hold the two 8-pixel halves of the same channel;
+  // the two row halves write separate slabs (2 * split + wrow)
+  if (dob) {
+#pragma unroll
+    for (int j = 0; j < TMO; ++j) {
+      const float t = bsum[j] + __shfl_xor(bsum[j], 32, 64);
+      const int co = c0 + wco * 32 * TMO + 32 * j + (lane & 31);
+      if (lane < 32 && co < p.cout) p.bws[(long long)(2 * split + wrow) * p.cout + co] = t;
     }
   }
 
@@ -336,6 +367,8 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
     return tq * 128 + ch * 16 + (col & 7) * 2 + 8 * 128 * (grp >> 1);
   };
   const int wco = wave >> 2, wci = wave & 3;
+  const bool dob = p.bws != nullptr && k0 == 0 && wci == 0;  // bias column sums, as in wgrad_halo_kernel
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
   int g_off[4], x_off[2];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -370,6 +403,10 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
       bf16x8 a[4], b[2];
 #pragma unroll
       for (int j = 0; j < 4; ++j) a[j] = tr_pair(G + g_off[j] + r, G + g_off[j] + r + 4 * 128);
+      if (dob) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bsum[j] += sum8_bf16(a[j]);
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i) b[i] = tr_pair(X + x_off[i] + r, X + x_off[i] + r + 4 * 128);
 #pragma unroll
@@ -379,6 +416,14 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+  }
+  if (dob) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = bsum[j] + __shfl_xor(bsum[j], 32, 64);
+      const int co = c0 + wco * 128 + 32 * j + (lane & 31);
+      if (lane < 32 && co < p.cout) p.bws[(long long)split * p.cout + co] = t;
+    }
   }
   // partial slab ws[split][co][ci]; C layout: column (ci) = lane & 31, rows (co) =
   // 8*(e>>2) + 4*(lane>>5) + (e&3)
@@ -470,6 +515,12 @@ static const int wg_merge = getenv("DVIE_WG_MERGE") && *getenv("DVIE_WG_MERGE") 
 // DVIE_SETPRIO=1: s_setprio 1 for the second half of the waves in the halo conv / weight-gradient
 // kernels (A/B runs)
 static const int wg_setprio = getenv("DVIE_SETPRIO") && *getenv("DVIE_SETPRIO") == '1' ? 2 : 0;
+
+// bias partial slabs the halo kernels write to p.bws (0: the launch is not theirs)
+int wgrad_halo_bias_slabs(const dvie_wgrad_desc& p) {
+  if (!wgrad_halo_eligible(p)) return 0;
+  return wgrad_plan(p).wide ? p.splits : 2 * p.splits;
+}
 
 int wgrad_halo_slabs(const dvie_wgrad_desc& p) {
   return wgrad_halo_eligible(p) && !wg_merge && !wgrad_plan(p).wide ? 2 * p.splits : p.splits;

@@ -1197,7 +1197,14 @@ class Plan:
             hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))  # the halo kernel's preferred split
             d.splits = hint if hint > 0 else splits
             slabs = lib.dvie_wgrad_slabs(ctypes.byref(d))
-            self.ws_floats = max(self.ws_floats, slabs * lay.cout_p * ntap * x.c)
+            wfl = slabs * lay.cout_p * ntap * x.c
+            bslabs = 0
+            if lay.has_bias:  # bias column sums ride on the weight-gradient launch (d.bws)
+                d.bws = 1  # placeholder (set in _finalize): makes the query see a bias launch
+                bslabs = lib.dvie_wgrad_bias_slabs(ctypes.byref(d))
+                d.bws = None
+                o.bws_off = wfl
+            self.ws_floats = max(self.ws_floats, wfl + bslabs * lay.cout_p)
             o.meta = dict(cls="conv_wgrad", name=lay.name, flops=2.0 * npix * lay.cout * lay.cin * ntap,
                           bytes=float(self.es * (npix * lay.cout + nb * x.H * x.W * lay.cin)
                                       + 4 * slabs * lay.cout_p * ntap * x.c))
@@ -1212,18 +1219,13 @@ class Plan:
             self.bwd.append(o)
             self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
             if lay.has_bias:
-                csplits = max(1, min(2048, npix // 512))  # >= 8 blocks per CU at full resolution
-                o = self._op(L.OP_COLSUM)
-                cd = o.u.colsum
-                cd.g, cd.ws, cd.g_ld, cd.rows, cd.c, cd.splits, cd.dtype = gout, 0, gld, npix, lay.cout_p, csplits, self.dt
-                self.ws_floats = max(self.ws_floats, csplits * lay.cout_p)
-                self.bwd.append(o)
                 o = self._op(L.OP_WREDUCE)
                 r = o.u.wreduce
                 r.ws, r.dw, r.cmap = 0, 0, None
-                r.splits, r.ws_rows, r.ws_k, r.co_off = csplits, lay.cout_p, 1, 0
+                r.splits, r.ws_rows, r.ws_k, r.co_off = bslabs, lay.cout_p, 1, 0
                 r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
                 r.beta = 0 if first else 1
+                o.ws_off = wfl
                 self.bwd.append(o)
                 self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
             self.wg_first[lay] = True
@@ -1381,10 +1383,12 @@ class Plan:
         for o in self.bwd:
             if o.kind == L.OP_WGRAD:
                 o.u.wgrad.ws = self.ws.data_ptr()
+                if hasattr(o, "bws_off"):  # bias partials after the weight slabs
+                    o.u.wgrad.bws = self.ws.data_ptr() + 4 * o.bws_off
             elif o.kind == L.OP_COLSUM:
                 o.u.colsum.ws = self.ws.data_ptr()
             elif o.kind == L.OP_WREDUCE:
-                o.u.wreduce.ws = self.ws.data_ptr()
+                o.u.wreduce.ws = self.ws.data_ptr() + 4 * getattr(o, "ws_off", 0)
         # pack op (all layers, one launch) goes first in the forward list
         descs = self._pack_descs
         if not descs:  # no convolutions (e.g. a pointwise-only plan)

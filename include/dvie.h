@@ -102,9 +102,17 @@ typedef struct dvie_wgrad_desc {
   int sx, th, tw, dy0;
   int dx0, ddy, ddx, splits;
   int dtype, pad0;
+  float* bws; /* NULL, or the bias-gradient partials: bws[slab][cout] = column sums of g over
+                 the slab's pixels (dvie_wgrad_bias_slabs slabs; reduce them with
+                 dvie_wgrad_reduce, ws_k = 1).  The halo weight-gradient kernels sum g while
+                 they hold it for the MFMAs (no second pass over g); other launches run a
+                 column-sum pass.  Replaces the separate nn.Conv2d bias backward. */
 } dvie_wgrad_desc;
 
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream);
+
+/* Number of bias partial slabs dvie_conv2d_wgrad writes to d->bws. */
+int dvie_wgrad_bias_slabs(const dvie_wgrad_desc* d);
 
 /* Split count the library prefers for this weight gradient (0: no preference).  bf16
  * stride-1 1x1/3x3 convs with c and cout multiples of 64 run a halo-tile kernel that
