@@ -36,13 +36,17 @@ __device__ __forceinline__ bf16x8 tr_pair(const char* p0, const char* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// sum of a fragment's 8 bf16 values in fp32 (bias column sums)
-__device__ __forceinline__ float sum8_bf16(const bf16x8 v) {
+// t + the sum of a fragment's 8 bf16 values, in fp32: four v_dot2c_f32_bf16 against (1, 1)
+// (bias column sums)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float sum8_bf16(const bf16x8 v, float t) {
   const i32x4 u = __builtin_bit_cast(i32x4, v);
-  float t = 0.f;
+  const bf16x2_t one = __builtin_bit_cast(bf16x2_t, 0x3F803F80);
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
-    t += __uint_as_float(((uint32_t)u[e]) << 16) + __uint_as_float(((uint32_t)u[e]) & 0xffff0000u);
+  for (int e = 0; e < 4; ++e) {
+    const int w = u[e];  // (a bit_cast of the vector element itself reads element 0 on this compiler)
+    t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, w), one, t, false);
+  }
   return t;
 }
 
@@ -230,10 +234,6 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
         bf16x8 a[TMO];
 #pragma unroll
         for (int j = 0; j < TMO; ++j) a[j] = tr_pair(G + g_off[j] + gr * 128, G + g_off[j] + gr * 128 + 4 * 128);
-        if (dob) {
-#pragma unroll
-          for (int j = 0; j < TMO; ++j) bsum[j] += sum8_bf16(a[j]);
-        }
 #pragma unroll
         for (int ti = 0; ti < TH; ++ti) {
           const int slot = (T.y0 + py + ti) % C::R;  // ring slot of halo row py + ti (uniform)
@@ -254,6 +254,10 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
             }
           }
         }
+        // every wave sums (4 VALU per fragment, no branch to split the k-step's schedule);
+        // only the dob waves write the result
+#pragma unroll
+        for (int j = 0; j < TMO; ++j) bsum[j] = sum8_bf16(a[j], bsum[j]);
       }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -403,16 +407,14 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
       bf16x8 a[4], b[2];
 #pragma unroll
       for (int j = 0; j < 4; ++j) a[j] = tr_pair(G + g_off[j] + r, G + g_off[j] + r + 4 * 128);
-      if (dob) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bsum[j] += sum8_bf16(a[j]);
-      }
 #pragma unroll
       for (int i = 0; i < 2; ++i) b[i] = tr_pair(X + x_off[i] + r, X + x_off[i] + r + 4 * 128);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[j], b[i], acc[j][i], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bsum[j] = sum8_bf16(a[j], bsum[j]);  // (unconditional, as above)
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
