@@ -78,13 +78,15 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 }
 
 // 8 waves: (co half, ci half, row half); the two row halves accumulate separately and are
-// summed through LDS into one partial slab per split.
-template <int TH, int TW, int PR, int TMO, int TMI>
-__global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
-                                                         int tiles_x, int tiles_y, int n_tiles, int flags) {
+// summed through LDS into one partial slab per split.  NW = 4 (output channels <= 32, the
+// 448 -> 3 / 448 -> 20 heads): no co half -- the second half's waves would only multiply the
+// zero padding of channels 32..63, and without them each wave has its SIMD's MFMA pipe alone.
+template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
+                                                             int tiles_x, int tiles_y, int n_tiles, int flags) {
   typedef WgCfg<TH, TW, PR, TMO, TMI> C;
   static_assert(PR % 2 == 0, "row halves");
-  constexpr int NW = 8;
+  static_assert(NW == 8 || (NW == 4 && TMO == 1), "4-wave form: one 32-channel co block");
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(512) void wgrad_halo_kernel(const dvie_wgrad_desc p
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[a][e] = 0.f;
 
-  const int wco = (wave >> 1) & 1, wci = wave & 1, wrow = wave >> 2;
+  const int wco = NW == 8 ? (wave >> 1) & 1 : 0, wci = wave & 1, wrow = NW == 8 ? wave >> 2 : wave >> 1;
   // bias gradient (p.bws): the ci-block-0 workgroups' wci = 0 waves sum the G fragments they
   // already hold for the MFMAs (lane l: co = l % 32 of the fragment, 8 pixels)
   const bool dob = p.bws != nullptr && kb == 0 && wci == 0;
@@ -470,6 +472,9 @@ struct WgPlan {
   int pr, tmo, tmi, wide;
 };
 
+// DVIE_WG_NARROW=0: 3x3 layers with <= 32 output channels on the 8-wave kernel (A/B runs)
+static const bool wg_narrow_env_off = getenv("DVIE_WG_NARROW") && *getenv("DVIE_WG_NARROW") == '0';
+
 // DVIE_WG_WIDE=0: 1x1 wide layers on the 128 x 128 block kernel (A/B runs)
 static const bool wg_wide_env_off = getenv("DVIE_WG_WIDE") && *getenv("DVIE_WG_WIDE") == '0';
 
@@ -541,7 +546,10 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
   hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
                      tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio)
-  if (p.th == 3)
+  if (p.th == 3 && p.cout <= 32 && !wg_narrow_env_off)
+    hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 4, 1, 1, 4>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
+                       tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
+  else if (p.th == 3)
     DVIE_WG(3, 4, 1, 1);
   else if (w.tmo == 2 && w.tmi == 2)
     DVIE_WG(1, 2, 2, 2);

@@ -31,6 +31,15 @@ PROFILE = None  # set to a list to time every op with HIP events (bench profilin
 DEBUG_NAN = bool(os.environ.get("DVIE_DEBUG_NAN"))  # op-by-op non-finite tracing (diagnostics only)
 
 
+def _reduce_meta(name, r):
+    """profiling meta of a slab reduction: the partial slabs read once, the gradient
+    written (and read when accumulating)."""
+    rows = r.ws_rows - r.co_off
+    out = r.cout_p * r.cin_p * r.kh_n * r.kw_n
+    return dict(cls="wgrad_reduce", name=name, flops=0.0,
+                bytes=float(4 * (r.splits * rows * r.ws_k + out * (1 + r.beta))))
+
+
 def rup(x, m):
     return (x + m - 1) // m * m
 
@@ -1216,6 +1225,7 @@ class Plan:
             r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
             first = lay not in self.wg_first
             r.beta = 0 if first else 1
+            o.meta = _reduce_meta(lay.name, r)
             self.bwd.append(o)
             self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
             if lay.has_bias:
@@ -1225,6 +1235,7 @@ class Plan:
                 r.splits, r.ws_rows, r.ws_k, r.co_off = bslabs, lay.cout_p, 1, 0
                 r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
                 r.beta = 0 if first else 1
+                o.meta = _reduce_meta(lay.name + ".bias", r)
                 o.ws_off = wfl
                 self.bwd.append(o)
                 self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
