@@ -1281,6 +1281,8 @@ static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
 // DVIE_CONV_NK=0: narrow-input 3x3 convs on the chunked kernels (A/B runs)
 static const bool nk_env_off = getenv("DVIE_CONV_NK") && *getenv("DVIE_CONV_NK") == '0';
 
+bool conv_narrow_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_narrow.hip
+
 // Returns true when the halo kernel took the launch.
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   if (p.dtype != DVIE_BF16) return false;
@@ -1315,6 +1317,9 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
     }
     return true;
   }
+  // <= 32 output channels from > 64 input channels (the HRNet heads): one step per 32-channel
+  // chunk with all 9 taps (conv_narrow.hip)
+  if (t3 && cfg == -3 && conv_narrow_launch(p, s)) return true;
   if (cfg < 0) {  // measured on MI355X (tools/conv_tune.py): see DESIGN.md
     if (p.cout <= 32)
       cfg = 2;

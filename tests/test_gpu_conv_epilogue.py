@@ -120,6 +120,27 @@ def test_conv_strip_modes(dev, shape, mode, strip, monkeypatch):
     assert err < 1e-2, (shape, mode, strip, err)
 
 
+NARROW_SHAPES = [  # 3x3, <= 32 output channels from > 64 input channels: conv_narrow.hip
+    (2, 35, 90, 448, 24, 3),    # the seg head's channels, ragged rows and columns
+    (1, 33, 77, 96, 8, 3),      # the rgb head's padded 8 channels, 3 chunks, partial tiles
+    (3, 16, 128, 128, 32, 3),   # a full 32-channel block, 2 tiles per row, more tiles than rows
+]
+
+
+@pytest.mark.parametrize("out_f32", [False, True])
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", NARROW_SHAPES)
+def test_conv_narrow_modes(dev, shape, mode, out_f32, monkeypatch):
+    """The narrow-output kernel (one step per 32-channel chunk with all 9 taps) and, for
+    comparison, the chunked halo kernel it replaces (DVIE_CONV_NARROW=0): every epilogue
+    operand set, bf16 and fp32 output."""
+    errs = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("DVIE_CONV_NARROW", env)
+        errs[env] = _run(dev, shape, mode, out_f32=out_f32)
+    assert errs["1"] < 1e-2 and errs["0"] < 1e-2, (shape, mode, errs)
+
+
 @pytest.mark.parametrize("mode", ["none", "res+beta+z"])
 @pytest.mark.parametrize("strip", ["0", "1"])
 def test_conv_strip_fp32_out(dev, mode, strip, monkeypatch):
