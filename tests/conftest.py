@@ -9,8 +9,20 @@ for p in (ROOT, os.path.join(ROOT, "tests", "golden")):
         sys.path.insert(0, p)
 
 
+_HB_STREAM = None
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+    # pytest's fd-level capture redirects fd 2 (sys.__stderr__ included) while a test runs:
+    # the heartbeat writes to a duplicate of the fd 2 pytest saved before capturing
+    global _HB_STREAM
+    try:
+        capman = config.pluginmanager.getplugin("capturemanager")
+        fd = capman._global_capturing.err.targetfd_save
+        _HB_STREAM = os.fdopen(os.dup(fd), "w")
+    except Exception:
+        _HB_STREAM = None
 
 
 def gpu_available():
@@ -54,8 +66,8 @@ def _heartbeat(request):
 
     def beat():
         while not stop.wait(60):
-            print(f"[heartbeat] {request.node.nodeid} running {time.time() - t0:.0f}s", file=sys.__stderr__,
-                  flush=True)
+            print(f"[heartbeat] {request.node.nodeid} running {time.time() - t0:.0f}s",
+                  file=_HB_STREAM or sys.__stderr__, flush=True)
 
     th = threading.Thread(target=beat, daemon=True)
     th.start()
