@@ -21,6 +21,7 @@ EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW, EW_M
 LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC, LOSS_COSNHWC, LOSS_IOU, LOSS_ARGMAX_IOU = range(9)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
 OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD, OP_ATTN = 8, 9, 10, 11, 12
+OP_FORK, OP_JOIN = 13, 14  # branch-region markers of the op-list executor (dvie_op.lane)
 (ATTN_L2NORM, ATTN_L2NORM_BWD, ATTN_CORR, ATTN_GATHER, ATTN_GATHER_T, ATTN_SOFTMAX, ATTN_SOFTMAX_BWD, ATTN_WNORM,
  ATTN_WNORM_BWD, ATTN_POOL, ATTN_POOL_T) = range(11)
 
@@ -186,7 +187,7 @@ class _OpUnion(ctypes.Union):
 
 
 class Op(ctypes.Structure):
-    _fields_ = [("kind", i32), ("pad0", i32), ("u", _OpUnion)]
+    _fields_ = [("kind", i32), ("lane", i32), ("u", _OpUnion)]
 
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "common.h"
 
@@ -614,24 +615,178 @@ int dvie_scale(float* p, long long n, float s, void* stream) {
   DVIE_RETURN_LAUNCH();
 }
 
+}  // extern "C"
+
+// Lanes of the op-list executor (dvie_op.lane, include/dvie.h): lane 0 is the caller's
+// stream; lanes 1..7 are side streams of the current device, created on first use at the
+// default (lowest) priority, as the caller's stream.  Events are re-recorded at every use:
+// a stream wait binds to the record that precedes it.
+namespace {
+constexpr int kLanes = 8;
+struct DevLanes {
+  hipStream_t s[kLanes] = {};
+  hipEvent_t join[kLanes] = {};
+  hipEvent_t fork = nullptr, tail = nullptr;
+  bool ok = false;
+};
+std::mutex lanes_mu;
+DevLanes dev_lanes[64];
+
+DevLanes* lanes_of_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(lanes_mu);
+  DevLanes& d = dev_lanes[dev];
+  if (!d.ok) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    for (int l = 1; l < kLanes; ++l) {
+      if (hipStreamCreateWithPriority(&d.s[l], hipStreamNonBlocking, least) != hipSuccess ||
+          hipEventCreateWithFlags(&d.join[l], hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    }
+    if (hipEventCreateWithFlags(&d.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d.tail, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    d.ok = true;
+  }
+  return &d;
+}
+
+bool lanes_on() {
+  const char* e = getenv("DVIE_OP_LANES");
+  return !(e && *e == '0');
+}
+
+// per-call lane bookkeeping
+struct LaneRun {
+  DevLanes* d = nullptr;
+  hipStream_t main = nullptr;
+  int data_lane = 0;          // lane of the last non-weight-lane op
+  bool tail_fresh = false;    // lane 1 already waits for the data lane's current position
+  bool fork_valid = false;    // d->fork holds this call's current fork point
+  bool waited[kLanes] = {};   // branch lane waits on the current fork point
+  bool in_region[kLanes] = {};
+  bool used[kLanes] = {};
+
+  hipStream_t st(int l) const { return l == 0 ? main : d->s[l]; }
+
+  hipError_t join_lane(int l) {
+    hipError_t e = hipEventRecord(d->join[l], d->s[l]);
+    return e == hipSuccess ? hipStreamWaitEvent(main, d->join[l], 0) : e;
+  }
+  // FORK: the branch lanes' next ops wait for everything issued on the caller's stream so far
+  hipError_t fork() {
+    for (int l = 2; l < kLanes; ++l) waited[l] = false;
+    fork_valid = true;
+    data_lane = 0;
+    return hipEventRecord(d->fork, main);
+  }
+  // JOIN: the caller's stream waits for the branch lanes used since the fork
+  hipError_t join_region() {
+    hipError_t e = hipSuccess;
+    for (int l = 2; l < kLanes && e == hipSuccess; ++l)
+      if (in_region[l]) {
+        e = join_lane(l);
+        in_region[l] = false;
+      }
+    data_lane = 0;
+    tail_fresh = false;
+    return e;
+  }
+  // stream for an op of lane l (waits inserted as needed)
+  hipError_t enter(int l, hipStream_t* out) {
+    hipError_t e = hipSuccess;
+    if (l == 1) {
+      if (!tail_fresh) {  // the weight lane follows the data lane that produced its inputs
+        e = hipEventRecord(d->tail, st(data_lane));
+        if (e == hipSuccess) e = hipStreamWaitEvent(d->s[1], d->tail, 0);
+        tail_fresh = true;
+      }
+    } else {
+      if (l >= 2 && !waited[l]) {
+        if (!fork_valid) e = fork();  // branch ops without a FORK in this call: fork here
+        if (e == hipSuccess) e = hipStreamWaitEvent(d->s[l], d->fork, 0);
+        waited[l] = true;
+      }
+      if (l >= 2) in_region[l] = true;
+      data_lane = l;
+      tail_fresh = false;
+    }
+    used[l] = true;
+    *out = st(l);
+    return e;
+  }
+  hipError_t finish() {
+    hipError_t e = hipSuccess;
+    for (int l = 1; l < kLanes && e == hipSuccess; ++l)
+      if (used[l]) e = join_lane(l);
+    return e;
+  }
+};
+}  // namespace
+
+extern "C" {
+
 int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
+  LaneRun lr;
+  lr.main = (hipStream_t)stream;
+  const bool lanes = lanes_on();
+  auto finish = [&](int rc) {
+    if (lr.d) {
+      const hipError_t e = lr.finish();
+      if (rc == DVIE_OK && e != hipSuccess) {
+        set_error("run_ops: lane join failed");
+        return (int)e;
+      }
+    }
+    return rc;
+  };
   for (int i = 0; i < n; ++i) {
     int rc = DVIE_OK;
     const dvie_op& o = ops[i];
+    if (o.lane < 0 || o.lane >= kLanes) {
+      set_error("run_ops: lane %d of op %d out of range", o.lane, i);
+      return finish(DVIE_EINVAL);
+    }
+    const bool marker = o.kind == DVIE_OP_FORK || o.kind == DVIE_OP_JOIN;
+    hipStream_t st = lr.main;
+    if (lanes && (o.lane != 0 || marker)) {
+      if (!lr.d) lr.d = lanes_of_device();
+      if (!lr.d) {
+        set_error("run_ops: side streams unavailable");
+        return finish(DVIE_EINVAL);
+      }
+      hipError_t e = hipSuccess;
+      if (o.kind == DVIE_OP_FORK)
+        e = lr.fork();
+      else if (o.kind == DVIE_OP_JOIN)
+        e = lr.join_region();
+      else
+        e = lr.enter(o.lane, &st);
+      if (e != hipSuccess) {
+        set_error("run_ops: lane fork / join failed at op %d", i);
+        return finish((int)e);
+      }
+    } else if (lr.d && !marker) {
+      lr.enter(0, &st);
+    }
+    if (marker) continue;
+    void* s = (void*)st;
     switch (o.kind) {
-      case DVIE_OP_CONV: rc = dvie_conv2d_fwd(&o.u.conv, stream); break;
-      case DVIE_OP_WGRAD: rc = dvie_conv2d_wgrad(&o.u.wgrad, stream); break;
-      case DVIE_OP_WREDUCE: rc = dvie_wgrad_reduce(&o.u.wreduce, stream); break;
-      case DVIE_OP_COLSUM: rc = dvie_colsum(&o.u.colsum, stream); break;
-      case DVIE_OP_EW: rc = dvie_ew(&o.u.ew, stream); break;
-      case DVIE_OP_LOSS: rc = dvie_loss(&o.u.loss, stream); break;
-      case DVIE_OP_PACK: rc = dvie_pack_weights(o.u.pack.descs_dev, o.u.pack.n, o.u.pack.max_elems, stream); break;
-      case DVIE_OP_BN_FWD: rc = dvie_bn_fwd(&o.u.bn, stream); break;
-      case DVIE_OP_BN_BWD: rc = dvie_bn_bwd(&o.u.bn, stream); break;
-      case DVIE_OP_HEAD_FWD: rc = dvie_head_fwd(&o.u.head, stream); break;
-      case DVIE_OP_HEAD_BWD: rc = dvie_head_bwd(&o.u.head, stream); break;
-      case DVIE_OP_ATTN: rc = dvie_attn(&o.u.attn, stream); break;
-      default: set_error("run_ops: unknown op kind %d at %d", o.kind, i); return DVIE_EINVAL;
+      case DVIE_OP_CONV: rc = dvie_conv2d_fwd(&o.u.conv, s); break;
+      case DVIE_OP_WGRAD: rc = dvie_conv2d_wgrad(&o.u.wgrad, s); break;
+      case DVIE_OP_WREDUCE: rc = dvie_wgrad_reduce(&o.u.wreduce, s); break;
+      case DVIE_OP_COLSUM: rc = dvie_colsum(&o.u.colsum, s); break;
+      case DVIE_OP_EW: rc = dvie_ew(&o.u.ew, s); break;
+      case DVIE_OP_LOSS: rc = dvie_loss(&o.u.loss, s); break;
+      case DVIE_OP_PACK: rc = dvie_pack_weights(o.u.pack.descs_dev, o.u.pack.n, o.u.pack.max_elems, s); break;
+      case DVIE_OP_BN_FWD: rc = dvie_bn_fwd(&o.u.bn, s); break;
+      case DVIE_OP_BN_BWD: rc = dvie_bn_bwd(&o.u.bn, s); break;
+      case DVIE_OP_HEAD_FWD: rc = dvie_head_fwd(&o.u.head, s); break;
+      case DVIE_OP_HEAD_BWD: rc = dvie_head_bwd(&o.u.head, s); break;
+      case DVIE_OP_ATTN: rc = dvie_attn(&o.u.attn, s); break;
+      default: set_error("run_ops: unknown op kind %d at %d", o.kind, i); return finish(DVIE_EINVAL);
     }
     if (rc != DVIE_OK) {
       if (rc == DVIE_EINVAL) {
@@ -640,10 +795,10 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
         snprintf(buf, sizeof(buf), "op %d (kind %d): %s", i, o.kind, dvie_last_error());
         set_error("%s", buf);
       }
-      return rc;
+      return finish(rc);
     }
   }
-  return DVIE_OK;
+  return finish(DVIE_OK);
 }
 
 size_t dvie_abi_sizeof(int which) {

@@ -18,6 +18,7 @@ Each list runs with a single host call (`dvie_run_ops`) on the current HIP strea
 All activations are NHWC buffers allocated once per (batch, height, width) plan; the
 kernels never allocate.  Reference semantics: nets/HRNet.py, nets/vgg.py, losses.py.
 """
+import contextlib
 import ctypes
 import math
 import os
@@ -29,6 +30,10 @@ from . import _lib as L
 PADC = 8  # channel padding granule (16-byte bf16 vectors)
 PROFILE = None  # set to a list to time every op with HIP events (bench profiling steps)
 DEBUG_NAN = bool(os.environ.get("DVIE_DEBUG_NAN"))  # op-by-op non-finite tracing (diagnostics only)
+# DVIE_WGRAD_LANE=0: weight gradients on the caller's stream with everything else (A/B runs;
+# read when a plan is compiled)
+def _wgrad_lane():
+    return os.environ.get("DVIE_WGRAD_LANE", "1") != "0"
 
 
 def _reduce_meta(name, r):
@@ -174,7 +179,22 @@ class ConvLayer:
 
 
 class _Op:
-    pass
+    lane = 0  # executor lane (dvie_op.lane): 0 the caller's stream, 2.. branch lanes
+
+
+class ForkOp(_Op):
+    """Start of a branch region: ops of different lanes until the matching JoinOp are
+    independent (no op of one lane reads a buffer another lane's op writes) and run on their
+    own streams (DVIE_OP_FORK / DVIE_OP_JOIN, include/dvie.h); the backward mirrors it."""
+    out = None
+    act = 0
+
+    def inputs(self):
+        return []
+
+
+class JoinOp(ForkOp):
+    """End of a branch region."""
 
 
 class ConvOp(_Op):
@@ -390,6 +410,7 @@ class Graph:
         self.layers = []
         self.outputs = {}
         self.n_l1 = 0
+        self.cur_lane = 0
 
     # ---------------- builder ----------------
     def buffer(self, name, H, W, C, dtype=None, external=False):
@@ -522,7 +543,24 @@ class Graph:
     def output(self, key, region, channels):
         self.outputs[key] = (region, channels)
 
+    # ---- branch regions (independent lanes; see ForkOp) ----
+    def fork(self):
+        self._add(ForkOp())
+
+    def join(self):
+        self._add(JoinOp())
+
+    @contextlib.contextmanager
+    def lane(self, k):
+        prev, self.cur_lane = self.cur_lane, k
+        try:
+            yield
+        finally:
+            self.cur_lane = prev
+
     def _add(self, op):
+        if not isinstance(op, ForkOp):
+            op.lane = self.cur_lane
         self.ops.append(op)
         if op.out is not None:
             op.out.buf.producers.append(op)
@@ -532,6 +570,23 @@ class Graph:
     # ---------------- compile ----------------
     def compile(self, n_fwd, device, n_bwd=None, backward=True):
         return Plan(self, n_fwd, n_fwd if n_bwd is None else n_bwd, device, backward)
+
+
+class _Ops(list):
+    """A plan's descriptor list: every appended descriptor takes the lane of the graph op
+    being lowered (Plan.cur_lane)."""
+
+    def __init__(self, plan):
+        super().__init__()
+        self.plan = plan
+
+    def append(self, o):
+        o.lane = self.plan.cur_lane
+        super().append(o)
+
+    def extend(self, ops):
+        for o in ops:
+            self.append(o)
 
 
 class Plan:
@@ -548,8 +603,9 @@ class Plan:
         self.busy = False
         self.generation = 0
         self._alloc()
-        self.fwd = []
-        self.bwd = []
+        self.cur_lane = 0  # lane of the graph op whose descriptors are being emitted
+        self.fwd = _Ops(self)
+        self.bwd = _Ops(self)
         self._l1_fwd = []  # (forward list index, level) of the VGG feature-L1 loss ops
         self.ext_in = {}  # key -> list of (op index, InputOp) for patching
         self.ext_out = {}
@@ -744,6 +800,10 @@ class Plan:
         g = self.g
         nf = self.nf
         for op in g.ops:
+            self.cur_lane = op.lane
+            if isinstance(op, ForkOp):  # (JoinOp included)
+                self.fwd.append(self._op(L.OP_JOIN if isinstance(op, JoinOp) else L.OP_FORK))
+                continue
             if isinstance(op, InputOp):
                 n0, cnt = self._part(op.part)
                 o = self.ew_desc(L.EW_NCHW, cnt, op.out.H, op.out.W, op.out.c, self.ptr(op.out, n0), op.out.buf.C)
@@ -1041,6 +1101,7 @@ class Plan:
     def _build_backward(self):
         g = self.g
         nb = self.nb
+        self.cur_lane = 0
         self.wg_first = {}
         self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
         self._uses_left = {}
@@ -1058,6 +1119,10 @@ class Plan:
             b.done = True
             b.dact_done = all(p.act == L.ACT_NONE for p in b.producers)  # else _ensure_dact at the producer
         for op in reversed(g.ops):
+            self.cur_lane = op.lane
+            if isinstance(op, ForkOp):  # the backward runs the region the other way round
+                self.bwd.append(self._op(L.OP_FORK if isinstance(op, JoinOp) else L.OP_JOIN))
+                continue
             if isinstance(op, OutNCHWOp):
                 continue
             if isinstance(op, HeadOp):
@@ -1391,7 +1456,14 @@ class Plan:
         # workspace for wgrad / colsum partials
         self.ws = torch.empty(max(1, self.ws_floats), dtype=torch.float32, device=self.device)
         self.keep.append(self.ws)
+        wlane = _wgrad_lane()
         for o in self.bwd:
+            # weight / bias gradients are off the data-gradient chain: they run on the
+            # executor's side stream (dvie_op.lane 1), forked where their output gradient is
+            # final and joined at the end of each dvie_run_ops call.  They are the only users
+            # of self.ws, and they stay in order on that one stream.
+            if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM) and wlane:
+                o.lane = 1
             if o.kind == L.OP_WGRAD:
                 o.u.wgrad.ws = self.ws.data_ptr()
                 if hasattr(o, "bws_off"):  # bias partials after the weight slabs

@@ -371,10 +371,19 @@ class HRNet(FlatParams, nn.Module):
         A = L
         nbr = mod.num_branches
         xs = list(xs)
+        # the branches' block chains are independent (each reads and writes only its own
+        # resolution's buffers): a branch region, branch i on executor lane 0 / i + 1
+        # (concurrent HIP streams, forward and backward; DVIE_BRANCH_LANES=0: one stream)
+        region = nbr > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+        if region:
+            g.fork()
         for i in range(nbr):
-            for k, blk in enumerate(mod.branches[i]):
-                assert blk.downsample is None
-                xs[i] = self._basic(g, blk, xs[i], f"{name}.branches.{i}.{k}")
+            with g.lane(0 if i == 0 or not region else i + 1):
+                for k, blk in enumerate(mod.branches[i]):
+                    assert blk.downsample is None
+                    xs[i] = self._basic(g, blk, xs[i], f"{name}.branches.{i}.{k}")
+        if region:
+            g.join()
         if nbr == 1:
             return xs
         H, W = xs[0].H, xs[0].W
@@ -465,10 +474,18 @@ class HRNet(FlatParams, nn.Module):
             g.conv(cat, self.rgb_layer[0], hr, act=A.ACT_LRELU, name="rgb_layer.0")
             hs = E.R(g.buffer("seg_hidden", H, W, last))
             g.conv(cat, self.seg_layer[0], hs, act=A.ACT_LRELU, name="seg_layer.0")
+        # the two 3x3 output convs read disjoint hidden maps (or halves) and write separate
+        # outputs: a branch region (their data gradients write disjoint halves too)
+        region = os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+        if region:
+            g.fork()
         rgb = g.buffer("rgb", H, W, E.rup(self.rgb_out_dim, 8), dtype=torch.float32, external=True)
         g.conv(hr, self.rgb_layer[2], E.R(rgb), name="rgb_layer.2")
         seg = g.buffer("segout", H, W, E.rup(self.seg_out_dim, 8), dtype=torch.float32, external=True)
-        g.conv(hs, self.seg_layer[2], E.R(seg), name="seg_layer.2")
+        with g.lane(2 if region else 0):
+            g.conv(hs, self.seg_layer[2], E.R(seg), name="seg_layer.2")
+        if region:
+            g.join()
         g.output("rgb", E.R(rgb), self.rgb_out_dim)
         g.output("segout", E.R(seg), self.seg_out_dim)
 

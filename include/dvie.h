@@ -546,8 +546,22 @@ typedef struct dvie_attn_desc {
 int dvie_attn(const dvie_attn_desc* d, void* stream);
 
 /*
- * Op-list executor: runs n descriptors in order on one stream with a single host call
- * (the per-step forward and backward plans of the HRNet / VGG executors).
+ * Op-list executor: runs n descriptors in order with a single host call (the per-step
+ * forward and backward plans of the HRNet / VGG executors).  dvie_op.lane picks the stream:
+ *   0     the caller's stream;
+ *   1     the weight lane (a library side stream of the current device):
+ *         work off the critical path (weight gradients and their reductions).  A run of
+ *         lane-1 ops first waits for everything issued so far on the stream of the last
+ *         lane-0 / branch-lane op (the data lane that produced its inputs);
+ *   2..7  branch lanes (library side streams): independent branches of a network (HRNet's
+ *         resolution branches).  DVIE_OP_FORK (no payload) marks the start of a branch
+ *         region: each branch lane's first op after it waits for everything issued on the
+ *         caller's stream before the FORK; DVIE_OP_JOIN makes the caller's stream wait for
+ *         the branch lanes used since the FORK.  Lane-0 ops inside a region run on the
+ *         caller's stream as one of the branches.
+ * The call ends with the caller's stream waiting for every side stream it used, so the call
+ * as a whole is ordered on the caller's stream; it is capturable (forks and joins become
+ * graph edges).  DVIE_OP_LANES=0 runs every op on the caller's stream.
  */
 #define DVIE_OP_CONV 1
 #define DVIE_OP_WGRAD 2
@@ -561,6 +575,8 @@ int dvie_attn(const dvie_attn_desc* d, void* stream);
 #define DVIE_OP_HEAD_FWD 10
 #define DVIE_OP_HEAD_BWD 11
 #define DVIE_OP_ATTN 12
+#define DVIE_OP_FORK 13 /* branch-region markers (no payload), see above */
+#define DVIE_OP_JOIN 14
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
@@ -569,7 +585,7 @@ typedef struct dvie_pack_list {
 
 typedef struct dvie_op {
   int kind;
-  int pad0;
+  int lane; /* 0: caller's stream, 1: weight lane, 2..7: branch lanes (see above) */
   union {
     dvie_conv_desc conv;
     dvie_wgrad_desc wgrad;

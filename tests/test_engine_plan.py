@@ -141,3 +141,94 @@ def test_buckets_with_unstacked_heads(bucket_mb, monkeypatch):
     assert k == len(cuts)
     if bucket_mb <= 4:
         assert len(cuts) >= 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_branch_regions_are_independent(dtype, monkeypatch):
+    """HRNet's branch regions (ForkOp ... JoinOp, one executor lane per resolution branch
+    and per output head, include/dvie.h dvie_op.lane): in the forward graph and in the
+    compiled backward descriptors, no channel range one branch lane writes is read or
+    written by another branch lane inside the region (the weight lane, 1, only reads);
+    markers pair up in both lists; the weight-gradient ops are on the weight lane."""
+    monkeypatch.setenv("DVIE_BRANCH_LANES", "1")
+    monkeypatch.setenv("DVIE_WGRAD_LANE", "1")
+    hr = make().coarse_model
+    g = hr._lower(E.Graph(dtype), 32, 64)
+    plan = g.compile(2, torch.device("cpu"), backward=True)
+
+    def overlap(u, v):  # (tensor, c0, c1) accesses
+        return u[0] == v[0] and u[1] < v[2] and v[1] < u[2]
+
+    def check(groups):
+        for a in groups:
+            for b in groups:
+                if a != b:
+                    wa, (rb, wb) = groups[a][1], groups[b]
+                    bad = [(u, v) for u in wa for v in rb + wb if overlap(u, v)]
+                    assert not bad, (a, b, bad[:3])
+
+    # forward graph
+    n_regions, groups = 0, None
+    for op in g.ops:
+        if isinstance(op, E.JoinOp):
+            check(groups)
+            groups = None
+        elif isinstance(op, E.ForkOp):
+            n_regions += 1
+            groups = {}
+        elif groups is not None:
+            r, w = groups.setdefault(op.lane, ([], []))
+            r.extend((id(x.buf), x.c0, x.c0 + x.c) for x in op.inputs())
+            if op.out is not None:
+                w.append((id(op.out.buf), op.out.c0, op.out.c0 + op.out.c))
+    # stage 2 (2 branches), stage 3 (3 branches), the two output heads
+    assert n_regions == 3 and groups is None
+
+    # backward descriptors: pointers mapped to channel ranges of the plan's buffers
+    spans = []
+    for b in g.buffers:
+        for t in (b.t, b.g):
+            if t is not None:
+                spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), id(t), t.element_size(), b.C))
+
+    def acc(p, c):
+        if not p:
+            return None
+        for lo, hi, k, es, C in spans:
+            if lo <= p < hi:
+                c0 = (p - lo) // es % C
+                return (k, c0, c0 + c)
+        return None
+
+    kinds = [plan.bwd_arr[i].kind for i in range(plan.n_bwd)]
+    assert kinds.count(L.OP_FORK) == kinds.count(L.OP_JOIN) == 3
+    groups = None
+    for i in range(plan.n_bwd):
+        o = plan.bwd_arr[i]
+        if o.kind == L.OP_FORK:
+            assert groups is None
+            groups = {}
+            continue
+        if o.kind == L.OP_JOIN:
+            check(groups)
+            groups = None
+            continue
+        if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM):
+            assert o.lane == 1
+            continue
+        if groups is None:
+            assert o.lane == 0
+            continue
+        assert o.kind in (L.OP_CONV, L.OP_EW), o.kind
+        r, w = groups.setdefault(o.lane, ([], []))
+        if o.kind == L.OP_CONV:
+            d = o.u.conv
+            reads = [(d.x, d.c), (d.res, d.cout), (d.z, d.cout)] + ([(d.y, d.cout)] if d.beta else [])
+            w.append(acc(d.y, d.cout))
+        else:
+            d = o.u.ew
+            reads = [(d.src0, d.c), (d.src1, d.c), (d.src2, d.c), (d.res, d.c), (d.z, d.c)] + \
+                ([(d.y, d.c)] if d.beta else [])
+            w.append(acc(d.y, d.c))
+        r.extend(a for a in (acc(p, c) for p, c in reads) if a is not None)
+    assert groups is None
