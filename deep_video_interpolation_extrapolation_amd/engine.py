@@ -185,9 +185,14 @@ class _Op:
 class ForkOp(_Op):
     """Start of a branch region: ops of different lanes until the matching JoinOp are
     independent (no op of one lane reads a buffer another lane's op writes) and run on their
-    own streams (DVIE_OP_FORK / DVIE_OP_JOIN, include/dvie.h); the backward mirrors it."""
+    own streams (DVIE_OP_FORK / DVIE_OP_JOIN, include/dvie.h).  backward=True: the backward
+    mirrors the region (valid when every gradient the region's ops emit stays in the lane
+    that produced its inputs); False: the backward of its ops runs on lane 0."""
     out = None
     act = 0
+
+    def __init__(self, backward=True):
+        self.backward = backward
 
     def inputs(self):
         return []
@@ -544,11 +549,13 @@ class Graph:
         self.outputs[key] = (region, channels)
 
     # ---- branch regions (independent lanes; see ForkOp) ----
-    def fork(self):
-        self._add(ForkOp())
+    def fork(self, backward=True):
+        self._region = ForkOp(backward)
+        self._add(self._region)
 
     def join(self):
-        self._add(JoinOp())
+        self._add(JoinOp(self._region.backward))
+        self._region = None
 
     @contextlib.contextmanager
     def lane(self, k):
@@ -561,6 +568,8 @@ class Graph:
     def _add(self, op):
         if not isinstance(op, ForkOp):
             op.lane = self.cur_lane
+            reg = getattr(self, "_region", None)
+            op.bwd_lane = op.lane if reg is None or reg.backward else 0
         self.ops.append(op)
         if op.out is not None:
             op.out.buf.producers.append(op)
@@ -1119,9 +1128,10 @@ class Plan:
             b.done = True
             b.dact_done = all(p.act == L.ACT_NONE for p in b.producers)  # else _ensure_dact at the producer
         for op in reversed(g.ops):
-            self.cur_lane = op.lane
+            self.cur_lane = getattr(op, "bwd_lane", 0)
             if isinstance(op, ForkOp):  # the backward runs the region the other way round
-                self.bwd.append(self._op(L.OP_FORK if isinstance(op, JoinOp) else L.OP_JOIN))
+                if op.backward:
+                    self.bwd.append(self._op(L.OP_FORK if isinstance(op, JoinOp) else L.OP_JOIN))
                 continue
             if isinstance(op, OutNCHWOp):
                 continue

@@ -318,6 +318,11 @@ class HRNet(FlatParams, nn.Module):
         stages = [self.stage2, self.stage3] + ([self.stage4] if self.highres_large else [])
         for si, (tr, st) in enumerate(zip(trans, stages)):
             x_list = []
+            # several new branches read the same input: a forward-only branch region (their
+            # backwards sum into that input's gradient)
+            region = sum(t is not None for t in tr) > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+            if region:
+                g.fork(backward=False)
             for i, t in enumerate(tr):
                 if t is None:
                     x_list.append(y_list[i])
@@ -325,13 +330,16 @@ class HRNet(FlatParams, nn.Module):
                 # reference: transition1[i](x) (nets/HRNet.py:548-553), later transitions
                 # always read the last branch output (l.555-564)
                 cur = y_list[-1]
-                for j, seq in enumerate(t if isinstance(t[0], nn.Sequential) else [t]):
-                    conv = seq[0]
-                    hh, ww = _out_hw(conv, cur.H, cur.W)
-                    ob = g.buffer(f"trans{si}.{i}.{j}", hh, ww, conv.out_channels)
-                    g.conv(cur, conv, E.R(ob), act=A.ACT_LRELU, name=f"transition{si + 1}.{i}")
-                    cur = E.R(ob)
+                with g.lane(0 if i == 0 or not region else i + 1):
+                    for j, seq in enumerate(t if isinstance(t[0], nn.Sequential) else [t]):
+                        conv = seq[0]
+                        hh, ww = _out_hw(conv, cur.H, cur.W)
+                        ob = g.buffer(f"trans{si}.{i}.{j}", hh, ww, conv.out_channels)
+                        g.conv(cur, conv, E.R(ob), act=A.ACT_LRELU, name=f"transition{si + 1}.{i}")
+                        cur = E.R(ob)
                 x_list.append(cur)
+            if region:
+                g.join()
             last_stage = si == len(stages) - 1
             for mi, mod in enumerate(st):
                 x_list = self._hr_module(g, mod, x_list, f"stage{si + 2}.{mi}", final=last_stage and
@@ -392,42 +400,16 @@ class HRNet(FlatParams, nn.Module):
             last = sum(x.c for x in xs)
             cat = g.buffer("cat", H, W, last)
         ys = []
+        # the fused outputs are independent in the forward (each reads the branch outputs and
+        # writes its own buffers); their backwards sum into shared branch gradients, so the
+        # region is forward-only
+        if region:
+            g.fork(backward=False)
         for i in range(len(mod.fuse_layers)):
-            fl = mod.fuse_layers[i]
-            ups = []
-            for j in range(i + 1, nbr):
-                cv = fl[j][0]
-                t = g.buffer(f"{name}.fuse.{i}.{j}", xs[j].H, xs[j].W, cv.out_channels)
-                g.conv(xs[j], cv, E.R(t), name=f"{name}.fuse_layers.{i}.{j}")
-                ups.append(E.R(t))
-            downs = [j for j in range(i)]
-            if i == 0:
-                out = E.R(cat, 0, xs[0].c) if final else E.R(g.buffer(f"{name}.y{i}", H, W, xs[0].c))
-                self._fuse_many(g, [xs[0]] + ups, out, A.ACT_LRELU, f"{name}.pre{i}")
-                ys.append(out)
-                continue
-            base = xs[i]
-            if ups:
-                t = g.buffer(f"{name}.sum{i}", xs[i].H, xs[i].W, xs[i].c)
-                self._fuse_many(g, [xs[i]] + ups, E.R(t), A.ACT_NONE, f"{name}.pre{i}")
-                base = E.R(t)
-            acc = base
-            for jn, j in enumerate(downs):
-                seq = fl[j]
-                cur = xs[j]
-                for k in range(len(seq) - 1):
-                    cv = seq[k][0]
-                    hh, ww = _out_hw(cv, cur.H, cur.W)
-                    t = g.buffer(f"{name}.down.{i}.{j}.{k}", hh, ww, cv.out_channels)
-                    g.conv(cur, cv, E.R(t), act=A.ACT_LRELU, name=f"{name}.fuse_layers.{i}.{j}.{k}")
-                    cur = E.R(t)
-                cv = seq[len(seq) - 1][0]
-                lastj = jn == len(downs) - 1
-                t = g.buffer(f"{name}.y{i}" if lastj else f"{name}.acc{i}.{j}", xs[i].H, xs[i].W, xs[i].c)
-                g.conv(cur, cv, E.R(t), act=A.ACT_LRELU if lastj else A.ACT_NONE, res=acc,
-                       name=f"{name}.fuse_layers.{i}.{j}")
-                acc = E.R(t)
-            ys.append(acc)
+            with g.lane(0 if i == 0 or not region else i + 1):
+                ys.append(self._fuse_output(g, mod, xs, i, cat, final, name))
+        if region:
+            g.join()
         if not final:
             return ys
         # final upsample of every branch into the concat buffer
@@ -437,6 +419,47 @@ class HRNet(FlatParams, nn.Module):
             off += ys[i].c
         self._heads(g, E.R(cat))
         return ys
+
+    def _fuse_output(self, g, mod, xs, i, cat, final, name):
+        """Fused output i of a HighResolutionModule (nets/HRNet.py:209-225): the sum of
+        branch i and every other branch resized to it (1x1 conv + upsample from coarser
+        branches, strided 3x3 chains from finer ones), LeakyReLU."""
+        A = L
+        nbr = len(xs)
+        H, W = xs[0].H, xs[0].W
+        fl = mod.fuse_layers[i]
+        ups = []
+        for j in range(i + 1, nbr):
+            cv = fl[j][0]
+            t = g.buffer(f"{name}.fuse.{i}.{j}", xs[j].H, xs[j].W, cv.out_channels)
+            g.conv(xs[j], cv, E.R(t), name=f"{name}.fuse_layers.{i}.{j}")
+            ups.append(E.R(t))
+        if i == 0:
+            out = E.R(cat, 0, xs[0].c) if final else E.R(g.buffer(f"{name}.y{i}", H, W, xs[0].c))
+            self._fuse_many(g, [xs[0]] + ups, out, A.ACT_LRELU, f"{name}.pre{i}")
+            return out
+        base = xs[i]
+        if ups:
+            t = g.buffer(f"{name}.sum{i}", xs[i].H, xs[i].W, xs[i].c)
+            self._fuse_many(g, [xs[i]] + ups, E.R(t), A.ACT_NONE, f"{name}.pre{i}")
+            base = E.R(t)
+        acc = base
+        for j in range(i):
+            seq = fl[j]
+            cur = xs[j]
+            for k in range(len(seq) - 1):
+                cv = seq[k][0]
+                hh, ww = _out_hw(cv, cur.H, cur.W)
+                t = g.buffer(f"{name}.down.{i}.{j}.{k}", hh, ww, cv.out_channels)
+                g.conv(cur, cv, E.R(t), act=A.ACT_LRELU, name=f"{name}.fuse_layers.{i}.{j}.{k}")
+                cur = E.R(t)
+            cv = seq[len(seq) - 1][0]
+            lastj = j == i - 1
+            t = g.buffer(f"{name}.y{i}" if lastj else f"{name}.acc{i}.{j}", xs[i].H, xs[i].W, xs[i].c)
+            g.conv(cur, cv, E.R(t), act=A.ACT_LRELU if lastj else A.ACT_NONE, res=acc,
+                   name=f"{name}.fuse_layers.{i}.{j}")
+            acc = E.R(t)
+        return acc
 
     def _fuse_many(self, g, srcs, out, act, name):
         """sum of up to N multi-resolution terms as chained 3-input fuse kernels."""

@@ -168,21 +168,23 @@ def test_branch_regions_are_independent(dtype, monkeypatch):
                     assert not bad, (a, b, bad[:3])
 
     # forward graph
-    n_regions, groups = 0, None
+    n_regions, n_bwd_regions, groups = 0, 0, None
     for op in g.ops:
         if isinstance(op, E.JoinOp):
             check(groups)
             groups = None
         elif isinstance(op, E.ForkOp):
             n_regions += 1
+            n_bwd_regions += int(op.backward)
             groups = {}
         elif groups is not None:
             r, w = groups.setdefault(op.lane, ([], []))
             r.extend((id(x.buf), x.c0, x.c0 + x.c) for x in op.inputs())
             if op.out is not None:
                 w.append((id(op.out.buf), op.out.c0, op.out.c0 + op.out.c))
-    # stage 2 (2 branches), stage 3 (3 branches), the two output heads
-    assert n_regions == 3 and groups is None
+    # the branch blocks of stage 2 (2 branches) and stage 3 (3), the two output heads; in
+    # the forward only: transition1's two new branches, the fused outputs of stages 2 and 3
+    assert (n_regions, n_bwd_regions) == (6, 3) and groups is None
 
     # backward descriptors: pointers mapped to channel ranges of the plan's buffers
     spans = []
