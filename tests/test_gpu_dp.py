@@ -70,7 +70,8 @@ def _worker(rank, world, port, kind, q):
         ld = tr.step(mine)
         hr = tr.model.module.coarse_model
         torch.cuda.synchronize()
-        q.put((rank, hr._flat_grad.cpu().clone(), hr._flat.detach().cpu().clone(), float(ld["loss_all"])))
+        # numpy arrays travel by value (a shared tensor's fd would dangle once this process exits)
+        q.put((rank, hr._flat_grad.cpu().numpy().copy(), hr._flat.detach().cpu().numpy().copy(), float(ld["loss_all"])))
     except BaseException as e:
         q.put((rank, repr(e), None, None))
     finally:
@@ -88,7 +89,7 @@ def _dp_vs_single(dev, kind):
     res = {}
     for _ in range(world):
         r, g, flat, loss = q.get(timeout=400)
-        res[r] = (g, flat, loss)
+        res[r] = (g, flat, loss) if isinstance(g, str) else (torch.from_numpy(g), torch.from_numpy(flat), loss)
     for p in procs:
         p.join(timeout=60)
     for r in range(world):
@@ -142,8 +143,8 @@ def _graph_worker(rank, world, port, q):
         lb = float(gs.step()["loss_all"])
         torch.cuda.synchronize()
         ha, hb = a.model.module.coarse_model, b.model.module.coarse_model
-        q.put((rank, (la, lb, nev, ha._flat_grad.cpu(), hb._flat_grad.cpu(), ha._flat.detach().cpu(),
-                      hb._flat.detach().cpu())))
+        q.put((rank, (la, lb, nev) + tuple(t.detach().cpu().numpy().copy() for t in
+                                           (ha._flat_grad, hb._flat_grad, ha._flat, hb._flat))))
     except BaseException as e:
         q.put((rank, repr(e)))
     finally:
@@ -168,7 +169,7 @@ def test_graphed_dp2_step_overlaps_and_equals_eager(dev):
     for r in range(world):
         assert not isinstance(res[r], str), res[r]
     for r in range(world):
-        la, lb, nev, ga, gb, fa, fb = res[r]
+        la, lb, nev, ga, gb, fa, fb = res[r][:3] + tuple(torch.from_numpy(a) for a in res[r][3:])
         assert nev >= 3, nev  # 39.7 MB of HRNet gradients in 4 MB buckets
         assert abs(lb - la[-1]) <= 1e-5 * abs(la[-1]), (la, lb)
         rel = float((gb - ga).norm() / ga.norm())
