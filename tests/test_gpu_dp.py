@@ -168,8 +168,9 @@ def test_graphed_dp2_step_overlaps_and_equals_eager(dev):
         p.join(timeout=60)
     for r in range(world):
         assert not isinstance(res[r], str), res[r]
+    res = {r: v[:3] + tuple(torch.from_numpy(a) for a in v[3:]) for r, v in res.items()}
     for r in range(world):
-        la, lb, nev, ga, gb, fa, fb = res[r][:3] + tuple(torch.from_numpy(a) for a in res[r][3:])
+        la, lb, nev, ga, gb, fa, fb = res[r]
         assert nev >= 3, nev  # 39.7 MB of HRNet gradients in 4 MB buckets
         assert abs(lb - la[-1]) <= 1e-5 * abs(la[-1]), (la, lb)
         rel = float((gb - ga).norm() / ga.norm())
