@@ -1366,10 +1366,13 @@ class Plan:
         ph, wt, kpad = phase
         nb = self.nb
         npx = nb * ph["oh"] * ph["ow"]
-        buf = getattr(self, "_i2c", None)
-        if buf is None or buf.numel() < npx * kpad:  # one scratch for all such layers (one stream)
+        # one scratch per executor lane, shared by the layers of that lane (in order on its
+        # stream): the two heads' data gradients run on different lanes
+        scratch = self.__dict__.setdefault("_i2c", {})
+        buf = scratch.get(self.cur_lane)
+        if buf is None or buf.numel() < npx * kpad:
             buf = torch.empty(npx * kpad, dtype=self.dtype, device=self.device)
-            self._i2c = buf
+            scratch[self.cur_lane] = buf
             self.keep.append(buf)
         e = self.ew_desc(L.EW_IM2COL, nb, out.H, out.W, kpad, buf.data_ptr(), kpad,
                          srcs=[(gout, gld, ph["th"], ph["tw"]), (None, 0, ph["dy0"], ph["dx0"]),

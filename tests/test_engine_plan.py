@@ -143,8 +143,8 @@ def test_buckets_with_unstacked_heads(bucket_mb, monkeypatch):
         assert len(cuts) >= 2
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_branch_regions_are_independent(dtype, monkeypatch):
+@pytest.mark.parametrize("dtype,im2col", [(torch.float32, "0"), (torch.bfloat16, "0"), (torch.bfloat16, "1")])
+def test_branch_regions_are_independent(dtype, im2col, monkeypatch):
     """HRNet's branch regions (ForkOp ... JoinOp, one executor lane per resolution branch
     and per output head, include/dvie.h dvie_op.lane): in the forward graph and in the
     compiled backward descriptors, no channel range one branch lane writes is read or
@@ -152,6 +152,7 @@ def test_branch_regions_are_independent(dtype, monkeypatch):
     markers pair up in both lists; the weight-gradient ops are on the weight lane."""
     monkeypatch.setenv("DVIE_BRANCH_LANES", "1")
     monkeypatch.setenv("DVIE_WGRAD_LANE", "1")
+    monkeypatch.setenv("DVIE_IM2COL_DGRAD", im2col)  # (its scratch buffers must be per lane)
     hr = make().coarse_model
     g = hr._lower(E.Graph(dtype), 32, 64)
     plan = g.compile(2, torch.device("cpu"), backward=True)
@@ -192,6 +193,10 @@ def test_branch_regions_are_independent(dtype, monkeypatch):
         for t in (b.t, b.g):
             if t is not None:
                 spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), id(t), t.element_size(), b.C))
+    for t in plan.keep:  # scratch and packed weights: one range each
+        if isinstance(t, torch.Tensor) and t.numel():
+            spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), id(t), t.element_size(),
+                          1 << 40))
 
     def acc(p, c):
         if not p:
