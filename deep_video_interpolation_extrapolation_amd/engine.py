@@ -1681,10 +1681,14 @@ class Plan:
             L.check(lib.dvie_run_ops(base + start * sz, end - start, s), what)
             return
         for i in range(start, end):  # op-by-op with events (profiling steps only)
+            if arr[i].kind in (L.OP_FORK, L.OP_JOIN):
+                continue  # one stream here: the region markers order nothing
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            lane, arr[i].lane = arr[i].lane, 0  # on the timed stream: no fork / join in the timing
             e0.record()
             L.check(lib.dvie_run_ops(base + i * sz, 1, s), what)
             e1.record()
+            arr[i].lane = lane
             PROFILE.append((metas[i] if metas is not None else None, arr[i].kind, e0, e1))
 
     def run_forward(self, stream=None):

@@ -14,6 +14,6 @@ if [ "$2" != "skip-tests" ]; then
 fi
 timeout -k 10 420 python -u bench.py > $out/bench.json 2> $out/bench.err || { echo "bench failed"; tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
-timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o bench -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-steps 0 --graph 0 > $out/bench_prof.json 2> $out/bench_prof.err || { echo "rocprof failed"; tail -20 $out/bench_prof.err; exit 1; }
+DVIE_OP_LANES=0 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o bench -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-steps 0 --graph 0 > $out/bench_prof.json 2> $out/bench_prof.err || { echo "rocprof failed"; tail -20 $out/bench_prof.err; exit 1; }
 find $out/prof -name '*kernel_stats.csv' -exec head -12 {} \;
 echo done
