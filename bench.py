@@ -57,8 +57,11 @@ def parse():
                     help="c2: BASELINE configs[1] (InterNet 256x512 bf16, batch 8; the default line); c5: "
                          "BASELINE configs[4] per GPU (two-stage extrapolation ExtraStage3Net 1024x2048 bf16, batch "
                          "1, hipGraph-captured step)")
-    ap.add_argument("--graph", type=int, default=1, help="1: time the hipGraph-captured step (runners/graph.py), "
-                                                           "0: the eager step")
+    ap.add_argument("--graph", type=int, default=None,
+                    help="1: time the hipGraph-captured step (runners/graph.py), 0: the eager step; default 0 for "
+                         "c2 (same box, r03q: eager 216.4 vs captured 211.7 frames/s -- the graph replay runs the "
+                         "executor's side-stream lanes one after the other), 1 for c5 (the config names a "
+                         "captured step)")
     return ap.parse_args()
 
 
@@ -256,6 +259,8 @@ WORKLOAD_SHAPE = {"c2": dict(batch=8, height=256, width=512), "c5": dict(batch=1
 
 def main():
     a = parse()
+    if a.graph is None:
+        a.graph = 1 if a.workload == "c5" else 0
     for k, v in WORKLOAD_SHAPE[a.workload].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
@@ -425,7 +430,7 @@ def main():
                                     f"int_9_len_3 train step {a.height}x{a.width} {a.precision}" if c5 else
                                     f"InterNet int_5_len_3 train step {a.height}x{a.width} {a.precision}"),
                        "per_gpu_batch": a.batch, "global_batch": a.batch * world, "parallelism": f"dp{world}",
-                       "step": "hipGraph-captured" if a.graph else "eager"},
+                       "step": "hipGraph-captured" if a.graph else "eager, executor side-stream lanes"},
             "eager_ms_per_step": round(eager_dt * 1e3 / a.steps, 3),
             "roofline": roof,
             "loss_all": loss_all,
