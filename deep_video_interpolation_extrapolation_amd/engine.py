@@ -1050,7 +1050,12 @@ class Plan:
         pend = b.pending.setdefault(key, [])
         pend.append((emitter, ident))
         if len(pend) == b.expected[key]:
-            self._flush(b, key)
+            if self._region_open and id(b) in self._shared_in:
+                # read by several lanes of the region being mirrored: its contributions come
+                # from different lanes, so it is summed on lane 0 after the region's JOIN
+                self._deferred.append((b, key))
+            else:
+                self._flush(b, key)
 
     def _flush(self, b, key):
         c0, c = key
@@ -1107,10 +1112,28 @@ class Plan:
         self.bwd.append(self.ew_desc(L.EW_COPY, self.nb, out.H, out.W, out.c, gp, b.C, [(gp, b.C, out.H, out.W)],
                                      z=self.ptr(out), z_ld=b.C, dact=op.act))
 
+    def _shared_region_inputs(self):
+        """ids of the buffers that ops of more than one lane read inside a backward-mirrored
+        branch region (their gradients sum contributions from several lanes)."""
+        shared, lanes = set(), None
+        for op in self.g.ops:
+            if isinstance(op, JoinOp):
+                shared.update(k for k, ls in lanes.items() if len(ls) > 1)
+                lanes = None
+            elif isinstance(op, ForkOp):
+                lanes = {} if op.backward else None
+            elif lanes is not None:
+                for r in op.inputs():
+                    lanes.setdefault(id(r.buf), set()).add(op.lane)
+        return shared
+
     def _build_backward(self):
         g = self.g
         nb = self.nb
         self.cur_lane = 0
+        self._shared_in = self._shared_region_inputs()
+        self._region_open = False
+        self._deferred = []
         self.wg_first = {}
         self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
         self._uses_left = {}
@@ -1131,7 +1154,13 @@ class Plan:
             self.cur_lane = getattr(op, "bwd_lane", 0)
             if isinstance(op, ForkOp):  # the backward runs the region the other way round
                 if op.backward:
-                    self.bwd.append(self._op(L.OP_FORK if isinstance(op, JoinOp) else L.OP_JOIN))
+                    opening = isinstance(op, JoinOp)
+                    self.bwd.append(self._op(L.OP_FORK if opening else L.OP_JOIN))
+                    self._region_open = opening
+                    if not opening:  # every lane joined: the shared inputs' gradients
+                        for b, key in self._deferred:
+                            self._flush(b, key)
+                        self._deferred = []
                 continue
             if isinstance(op, OutNCHWOp):
                 continue

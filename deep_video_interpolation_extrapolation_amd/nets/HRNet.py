@@ -318,11 +318,11 @@ class HRNet(FlatParams, nn.Module):
         stages = [self.stage2, self.stage3] + ([self.stage4] if self.highres_large else [])
         for si, (tr, st) in enumerate(zip(trans, stages)):
             x_list = []
-            # several new branches read the same input: a forward-only branch region (their
-            # backwards sum into that input's gradient)
+            # several new branches read the same input: a branch region (their backwards sum
+            # into that input's gradient on lane 0 after the region)
             region = sum(t is not None for t in tr) > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
             if region:
-                g.fork(backward=False)
+                g.fork()
             for i, t in enumerate(tr):
                 if t is None:
                     x_list.append(y_list[i])
@@ -400,11 +400,11 @@ class HRNet(FlatParams, nn.Module):
             last = sum(x.c for x in xs)
             cat = g.buffer("cat", H, W, last)
         ys = []
-        # the fused outputs are independent in the forward (each reads the branch outputs and
-        # writes its own buffers); their backwards sum into shared branch gradients, so the
-        # region is forward-only
+        # the fused outputs are independent (each reads the branch outputs and writes its own
+        # buffers); in the backward the branch outputs' gradients, which sum contributions
+        # of every lane, are summed on lane 0 after the region (engine: shared region inputs)
         if region:
-            g.fork(backward=False)
+            g.fork()
         for i in range(len(mod.fuse_layers)):
             with g.lane(0 if i == 0 or not region else i + 1):
                 ys.append(self._fuse_output(g, mod, xs, i, cat, final, name))
