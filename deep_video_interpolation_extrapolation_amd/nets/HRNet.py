@@ -285,14 +285,22 @@ class HRNet(FlatParams, nn.Module):
         segs = []
         stem_c = 8 * F + rup(3 * F, 8) + self._stem_extra
         feat = g.buffer("feat", H, W, stem_c)
+        # the frames' segmentation encoders are independent chains into disjoint channel
+        # slices of the stem buffer: a branch region, one lane per frame
+        region = F > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+        if region:
+            g.fork()
         for k in range(F):
-            s_in = g.buffer(f"seg{k}_in", H, W, 24)
-            g.input_nchw(E.R(s_in), "seg", ext_c0=20 * k, ext_c=20)
-            e1 = g.buffer(f"seg{k}_e1", H, W, 32)
-            g.conv(E.R(s_in), self.seg_encoder[0], E.R(e1), act=A.ACT_ELU, name="seg_encoder.0")
-            e2 = g.buffer(f"seg{k}_e2", H, W, 32)
-            g.conv(E.R(e1), self.seg_encoder[2], E.R(e2), act=A.ACT_ELU, name="seg_encoder.2")
-            g.conv(E.R(e2), self.seg_encoder[4], E.R(feat, 8 * k, 8), name="seg_encoder.4")
+            with g.lane(0 if k == 0 or not region else k + 1):
+                s_in = g.buffer(f"seg{k}_in", H, W, 24)
+                g.input_nchw(E.R(s_in), "seg", ext_c0=20 * k, ext_c=20)
+                e1 = g.buffer(f"seg{k}_e1", H, W, 32)
+                g.conv(E.R(s_in), self.seg_encoder[0], E.R(e1), act=A.ACT_ELU, name="seg_encoder.0")
+                e2 = g.buffer(f"seg{k}_e2", H, W, 32)
+                g.conv(E.R(e1), self.seg_encoder[2], E.R(e2), act=A.ACT_ELU, name="seg_encoder.2")
+                g.conv(E.R(e2), self.seg_encoder[4], E.R(feat, 8 * k, 8), name="seg_encoder.4")
+        if region:
+            g.join()
         # xgrad: the frames input needs a gradient (ExtraTrainer rollout feeds a prediction back)
         g.input_nchw(E.R(feat, 8 * F, rup(3 * F, 8)), "x", ext_c=3 * F, requires_grad=xgrad)
         if self._stem_extra:  # decoded VAE feature (its gradient feeds the decoder backward)

@@ -183,9 +183,10 @@ def test_branch_regions_are_independent(dtype, im2col, monkeypatch):
             r.extend((id(x.buf), x.c0, x.c0 + x.c) for x in op.inputs())
             if op.out is not None:
                 w.append((id(op.out.buf), op.out.c0, op.out.c0 + op.out.c))
-    # the branch blocks of stage 2 (2 branches) and stage 3 (3), the two output heads,
-    # transition1's two new branches, the fused outputs of stages 2 and 3
-    assert (n_regions, n_bwd_regions) == (6, 6) and groups is None
+    # the two frames' segmentation encoders, the branch blocks of stage 2 (2 branches) and
+    # stage 3 (3), the two output heads, transition1's two new branches, the fused outputs of
+    # stages 2 and 3
+    assert (n_regions, n_bwd_regions) == (7, 7) and groups is None
 
     # backward descriptors: pointers mapped to channel ranges of the plan's buffers
     spans = []
@@ -208,7 +209,7 @@ def test_branch_regions_are_independent(dtype, im2col, monkeypatch):
         return None
 
     kinds = [plan.bwd_arr[i].kind for i in range(plan.n_bwd)]
-    assert kinds.count(L.OP_FORK) == kinds.count(L.OP_JOIN) == 6
+    assert kinds.count(L.OP_FORK) == kinds.count(L.OP_JOIN) == 7
     groups = None
     for i in range(plan.n_bwd):
         o = plan.bwd_arr[i]
