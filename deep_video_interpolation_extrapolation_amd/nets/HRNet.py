@@ -135,6 +135,13 @@ def _out_hw(conv, H, W):
     return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
 
 
+def _branch_lanes():
+    """DVIE_BRANCH_LANES=1: lower independent branches as branch regions (executor lanes 2..,
+    include/dvie.h).  Off by default: bit-identical, but measured neutral to -0.4% on the
+    bench step (same box, eager, profiles/r03v2/), while the weight lane alone gains."""
+    return os.environ.get("DVIE_BRANCH_LANES", "0") == "1"
+
+
 def _arg(args, name, default):
     return getattr(args, name, default) if args is not None else default
 
@@ -287,7 +294,7 @@ class HRNet(FlatParams, nn.Module):
         feat = g.buffer("feat", H, W, stem_c)
         # the frames' segmentation encoders are independent chains into disjoint channel
         # slices of the stem buffer: a branch region, one lane per frame
-        region = F > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+        region = F > 1 and _branch_lanes()
         if region:
             g.fork()
         for k in range(F):
@@ -328,7 +335,7 @@ class HRNet(FlatParams, nn.Module):
             x_list = []
             # several new branches read the same input: a branch region (their backwards sum
             # into that input's gradient on lane 0 after the region)
-            region = sum(t is not None for t in tr) > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+            region = sum(t is not None for t in tr) > 1 and _branch_lanes()
             if region:
                 g.fork()
             for i, t in enumerate(tr):
@@ -390,7 +397,7 @@ class HRNet(FlatParams, nn.Module):
         # the branches' block chains are independent (each reads and writes only its own
         # resolution's buffers): a branch region, branch i on executor lane 0 / i + 1
         # (concurrent HIP streams, forward and backward; DVIE_BRANCH_LANES=0: one stream)
-        region = nbr > 1 and os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+        region = nbr > 1 and _branch_lanes()
         if region:
             g.fork()
         for i in range(nbr):
@@ -507,7 +514,7 @@ class HRNet(FlatParams, nn.Module):
             g.conv(cat, self.seg_layer[0], hs, act=A.ACT_LRELU, name="seg_layer.0")
         # the two 3x3 output convs read disjoint hidden maps (or halves) and write separate
         # outputs: a branch region (their data gradients write disjoint halves too)
-        region = os.environ.get("DVIE_BRANCH_LANES", "1") != "0"
+        region = _branch_lanes()
         if region:
             g.fork()
         rgb = g.buffer("rgb", H, W, E.rup(self.rgb_out_dim, 8), dtype=torch.float32, external=True)
