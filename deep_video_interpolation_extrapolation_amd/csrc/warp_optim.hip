@@ -6,7 +6,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <mutex>
 
 #include "common.h"
 
@@ -618,8 +617,8 @@ int dvie_scale(float* p, long long n, float s, void* stream) {
 }  // extern "C"
 
 // Lanes of the op-list executor (dvie_op.lane, include/dvie.h): lane 0 is the caller's
-// stream; lanes 1..7 are side streams of the current device, created on first use at the
-// default (lowest) priority, as the caller's stream.  Events are re-recorded at every use:
+// stream; lanes 1..7 are side streams of the current device and host thread, created on
+// first use at the default (lowest) priority, as the caller's stream.  Events are re-recorded at every use:
 // a stream wait binds to the record that precedes it.
 namespace {
 constexpr int kLanes = 8;
@@ -629,13 +628,13 @@ struct DevLanes {
   hipEvent_t fork = nullptr, tail = nullptr;
   bool ok = false;
 };
-std::mutex lanes_mu;
-DevLanes dev_lanes[64];
+// per host thread (the forward and the autograd backward thread each get their own side
+// streams and events, so calls from two threads never re-record each other's events)
+thread_local DevLanes dev_lanes[64];
 
 DevLanes* lanes_of_device() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(lanes_mu);
   DevLanes& d = dev_lanes[dev];
   if (!d.ok) {
     int least = 0, greatest = 0;

@@ -549,7 +549,7 @@ int dvie_attn(const dvie_attn_desc* d, void* stream);
  * Op-list executor: runs n descriptors in order with a single host call (the per-step
  * forward and backward plans of the HRNet / VGG executors).  dvie_op.lane picks the stream:
  *   0     the caller's stream;
- *   1     the weight lane (a library side stream of the current device):
+ *   1     the weight lane (a library side stream of the current device and host thread):
  *         work off the critical path (weight gradients and their reductions).  A run of
  *         lane-1 ops first waits for everything issued so far on the stream of the last
  *         lane-0 / branch-lane op (the data lane that produced its inputs);
