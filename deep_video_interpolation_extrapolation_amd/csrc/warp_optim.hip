@@ -768,7 +768,11 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
         return finish((int)e);
       }
     } else if (lr.d && !marker) {
-      lr.enter(0, &st);
+      const hipError_t e = lr.enter(0, &st);
+      if (e != hipSuccess) {
+        set_error("run_ops: lane 0 entry failed at op %d", i);
+        return finish((int)e);
+      }
     }
     if (marker) continue;
     void* s = (void*)st;

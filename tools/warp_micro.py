@@ -59,7 +59,14 @@ def main():
                 run()
             e1.record()
             torch.cuda.synchronize()
-            print(f"{n}x{c}x{H}x{W} {tag}: {e0.elapsed_time(e1) / a.reps * 1e3:.1f} us/call", flush=True)
+            msg = f"{n}x{c}x{H}x{W} {tag}: {e0.elapsed_time(e1) / a.reps * 1e3:.1f} us/call"
+            if tag != "fwd":  # bit-level digest of the gradients (A/B runs of kernel variants)
+                import hashlib
+                h = hashlib.sha1()
+                for t in ((keep[5],) if tag == "bwd_dflow_only" else (dx, keep[5])):
+                    h.update(t.cpu().numpy().tobytes())
+                msg += f" digest {h.hexdigest()[:16]}"
+            print(msg, flush=True)
 
 
 if __name__ == "__main__":
