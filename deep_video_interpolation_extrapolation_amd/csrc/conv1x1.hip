@@ -644,7 +644,12 @@ bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
   // single K-step, 65-128 output channels: two 64-channel column tiles with every epilogue
   // operand prefetched beat one 128-channel tile (8x128x256 64->128: 33 vs 35 us residual,
   // 48 vs 56 us accumulate + activation input, tools/conv_epi_micro.py)
-  if (cfg < 0) cfg = cout <= 64 ? 100 : cout <= 128 ? (one ? 100 : 101) : wide;
+  // single K-step wide layers (layer1's 64->256 forward, the 256-channel data gradients of its
+  // 256->64 convs): 128-channel wave tiles of 4 accumulators with every epilogue operand
+  // prefetched (101) beat the 2-D wave grid's 8 (116): 213.5 -> 214.7 frames/s, 5 of 6 same-box
+  // pairs (profiles/r03wide1/); DVIE_CONV1X1_WIDE1 overrides it (A/B runs)
+  static const int wide1 = getenv("DVIE_CONV1X1_WIDE1") && *getenv("DVIE_CONV1X1_WIDE1") ? atoi(getenv("DVIE_CONV1X1_WIDE1")) : 101;
+  if (cfg < 0) cfg = cout <= 64 ? 100 : cout <= 128 ? (one ? 100 : 101) : one ? wide1 : wide;
   switch (cfg) {
     case 100: one ? launch_1x1<2, 1>(p, s) : launch_1x1<2, 3>(p, s); break;
     case 101: one ? launch_1x1<4, 1>(p, s) : launch_1x1<4, 3>(p, s); break;

@@ -33,6 +33,7 @@ CONV_CASES = [
     (20, 32, 3, 1, 16, 16, True),
     (32, 4, 3, 1, 16, 16, True),
     (448, 448, 1, 1, 8, 16, True),
+    (64, 256, 1, 1, 20, 36, False),
     (320, 272, 1, 1, 13, 21, False),
     (16, 96, 3, 1, 20, 70, True),
     (24, 448, 3, 1, 9, 130, False),
