@@ -257,7 +257,17 @@ def _free_port():
 WORKLOAD_SHAPE = {"c2": dict(batch=8, height=256, width=512), "c5": dict(batch=1, height=1024, width=2048)}
 
 
+def refuse_timing_switches(env=os.environ):
+    """Timing-only ablation switches (DVIE_*_DBG) skip stores, MFMAs or operand streams in the
+    kernels of a -DDVIE_TIMING_DBG build; a bench line must never run with one set."""
+    bad = sorted(k for k in env if k.startswith("DVIE_") and k.endswith("_DBG") and env[k] not in ("", "0"))
+    if bad:
+        print(f"bench.py: refusing to run with timing-only switches set: {', '.join(bad)}", file=sys.stderr)
+        sys.exit(2)
+
+
 def main():
+    refuse_timing_switches()
     a = parse()
     if a.graph is None:
         a.graph = 1 if a.workload == "c5" else 0

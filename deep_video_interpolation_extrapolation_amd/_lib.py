@@ -20,8 +20,7 @@ ACT_NONE, ACT_LRELU, ACT_ELU, ACT_RELU, ACT_TANH = 0, 1, 2, 3, 4
 EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW, EW_MASK, EW_IM2COL = range(10)
 LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC, LOSS_COSNHWC, LOSS_IOU, LOSS_ARGMAX_IOU = range(9)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
-OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD, OP_ATTN = 8, 9, 10, 11, 12
-OP_FORK, OP_JOIN = 13, 14  # branch-region markers of the op-list executor (dvie_op.lane)
+OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD, OP_ATTN, OP_HEAD3_BWD, OP_SEGENC_FWD = 8, 9, 10, 11, 12, 13, 14
 (ATTN_L2NORM, ATTN_L2NORM_BWD, ATTN_CORR, ATTN_GATHER, ATTN_GATHER_T, ATTN_SOFTMAX, ATTN_SOFTMAX_BWD, ATTN_WNORM,
  ATTN_WNORM_BWD, ATTN_POOL, ATTN_POOL_T) = range(11)
 
@@ -178,11 +177,31 @@ class PackList(ctypes.Structure):
     _fields_ = [("descs_dev", vp), ("n", i32), ("max_elems", i32)]
 
 
+class Head3BwdDesc(ctypes.Structure):
+    _fields_ = [
+        ("g", vp), ("h", vp), ("wd", vp), ("dh", vp), ("ws", vp),
+        ("g_ld", i64), ("h_ld", i64), ("dh_ld", i64),
+        ("n", i32), ("hgt", i32), ("wid", i32), ("c", i32),
+        ("cout", i32), ("kpad", i32), ("dy0", i32), ("dx0", i32),
+        ("splits", i32), ("dact", i32),
+        ("alpha", f32), ("pad0", f32),
+    ]
+
+
+class SegencDesc(ctypes.Structure):
+    _fields_ = [
+        ("inp", vp), ("e1", vp), ("e2", vp), ("out", vp), ("w0", vp), ("w2", vp), ("w4", vp),
+        ("b0", vp), ("b2", vp), ("b4", vp),
+        ("in_ld", i64), ("e1_ld", i64), ("e2_ld", i64), ("out_ld", i64),
+        ("n", i32), ("h", i32), ("w", i32), ("kpad0", i32), ("kpad2", i32), ("kpad4", i32),
+    ]
+
+
 class _OpUnion(ctypes.Union):
     _fields_ = [
         ("conv", ConvDesc), ("wgrad", WgradDesc), ("wreduce", WreduceDesc), ("colsum", ColsumDesc),
         ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList), ("bn", BnDesc), ("head", HeadDesc),
-        ("attn", AttnDesc),
+        ("attn", AttnDesc), ("head3", Head3BwdDesc), ("segenc", SegencDesc),
     ]
 
 
@@ -192,7 +211,7 @@ class Op(ctypes.Structure):
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
-        OP_ATTN: AttnDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
+        OP_ATTN: AttnDesc, OP_HEAD3_BWD: Head3BwdDesc, OP_SEGENC_FWD: SegencDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
 
 EXPORTS = [
     "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
@@ -201,7 +220,8 @@ EXPORTS = [
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
-    "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs",
+    "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs", "dvie_head3_bwd",
+    "dvie_segenc_fwd",
 ]
 
 _lib = None
@@ -235,7 +255,8 @@ def load():
         lib.dvie_last_error.restype = ctypes.c_char_p
         for name in ("dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_ew",
                      "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_head_fwd",
-                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_clip_prep", "dvie_attn"):
+                     "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_clip_prep", "dvie_attn",
+                     "dvie_head3_bwd", "dvie_segenc_fwd"):
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]

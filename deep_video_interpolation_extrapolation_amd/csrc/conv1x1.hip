@@ -94,6 +94,7 @@ struct G1Cfg {
 // MFMAs (1 residual, 2 accumulate target, 4 activation input).
 template <int TMC, int NS, int KC, int NWP, int MI, int NWC, bool OUTF32, int PRE = 0>
 __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv_desc p, int n_ct, int n_tiles, int dbg) {
+  dbg = DVIE_DBG(dbg);
   typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
   constexpr int NW = C::NW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
@@ -565,11 +566,15 @@ static bool persist_env_on() {
   return !(e && *e == '0');
 }
 
-// DVIE_1X1_DBG (timing only, wrong results): bit 1 skips the epilogue stores, bit 2 the
+// DVIE_1X1_DBG (timing only, wrong results; -DDVIE_TIMING_DBG builds only): bit 1 skips the epilogue stores, bit 2 the
 // MFMA loop (operand DMA kept); read per launch
 static int dbg_env() {
+#ifdef DVIE_TIMING_DBG
   const char* e = getenv("DVIE_1X1_DBG");
   return e && *e ? atoi(e) : 0;
+#else
+  return 0;
+#endif
 }
 
 // DVIE_1X1_PRE=0: no epilogue-operand prefetch (A/B runs); read per launch

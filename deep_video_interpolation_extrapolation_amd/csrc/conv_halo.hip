@@ -294,7 +294,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
   };
 
   // ---- prologue: job 0 halo (+ job 1 for 1x1), weights of steps 0 and 1 ----
-  const int dbg = epi_pre & 24;
+  const int dbg = DVIE_DBG(epi_pre & 24);
   epi_pre &= ~24;
   {
     const JobInfo J0 = tile_job(tile0);
@@ -509,8 +509,12 @@ static const int halo_setprio = getenv("DVIE_SETPRIO") && *getenv("DVIE_SETPRIO"
 // DVIE_HALO_WAIT=0: every step waits for all loads issued before it (A/B runs); read per launch
 static int halo_wait_flag() {
   const char* e = getenv("DVIE_HALO_WAIT");
+#ifdef DVIE_TIMING_DBG
   const char* d = getenv("DVIE_HALO_DBG");  // timing experiments only: 8 = no weight, 16 = no halo streaming
   return (e && *e == '0' ? 0 : 4) | (d && *d ? (atoi(d) & 24) : 0);
+#else
+  return e && *e == '0' ? 0 : 4;
+#endif
 }
 
 template <int TM, int WC, int WP, int TH, int TW>

@@ -61,6 +61,7 @@ __device__ __forceinline__ void narrow_act(float* v, int act, float alpha) {
 template <bool OUTF32>
 __global__ __launch_bounds__(512) void conv_narrow_kernel(const dvie_conv_desc p, int tiles_x, int tiles_y,
                                                           int n_tiles, int dbg) {
+  dbg = DVIE_DBG(dbg);
   typedef NarrowCfg C;
   constexpr int NW = C::NW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
@@ -301,10 +302,14 @@ static bool narrow_env_on() {
   return !(e && *e == '0');
 }
 
-// DVIE_NARROW_DBG (timing only, wrong results): bit 1 = no operand DMA, bit 2 = no MFMAs
+// DVIE_NARROW_DBG (timing only, wrong results; -DDVIE_TIMING_DBG builds only): bit 1 = no operand DMA, bit 2 = no MFMAs
 static int narrow_dbg() {
+#ifdef DVIE_TIMING_DBG
   const char* e = getenv("DVIE_NARROW_DBG");
   return e && *e ? atoi(e) : 0;
+#else
+  return 0;
+#endif
 }
 
 // Returns true when the narrow-output kernel took the launch.

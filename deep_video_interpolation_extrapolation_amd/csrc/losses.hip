@@ -525,7 +525,7 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
     DVIE_CHECK_ARG(d->grad == nullptr, "loss: kind %d is a metric (no gradient)", d->kind);
   hipStream_t s = (hipStream_t)stream;
   const LossPlan lp = plan_loss(*d);
-  const float vs = d->out_scale != 0.f ? d->out_scale : 1.f;
+  const float vs = d->out_scale;
   const int acc = d->out_acc;
   const double px = (double)d->bsz * d->h * d->w;
   const double tot = px * d->ch;

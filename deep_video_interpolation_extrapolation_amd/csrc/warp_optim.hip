@@ -11,6 +11,8 @@
 
 namespace dvie {
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
 // torch.linspace(-1, 1, n)[i] as computed by the CPU kernel (two-sided)
 __device__ __forceinline__ float linspace_pm1(int i, int n) {
   if (n <= 1) return -1.f;
@@ -164,6 +166,117 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
           warp_corners(im, t[k], p.w, a, b, cc, d, pair[k]);
           o[k] = warp_blend(a, b, cc, d, t[k]);
         }
+        store(c, o);
+      }
+    }
+  }
+}
+
+// Forward, two adjacent pixels per lane (CC = 3, even widths): a wave covers 512 consecutive
+// pixels of a row, lane owning the pairs (x, x + 1) at x = 2 lane + 128 k, k < 4.  Flow loads
+// and output stores are 8-byte pairs.  When (wave-uniform) every pair's two samples share
+// their corner rows and their corner columns fit in x0 .. x0 + 3 of the first one (a smooth
+// flow: neighbouring samples move together), ONE 16-byte load per corner row serves both
+// pixels of a pair: 2 gathers per channel for 2 pixels instead of 4, and half the flow-load
+// and store instructions.  Otherwise the pairs take the one-pixel corner loads.  The blend is
+// warp_blend's, so the outputs equal warp_fwd_kernel's bit for bit.
+template <int CC>
+__global__ __launch_bounds__(256) void warp_fwd2_kernel(const dvie_warp_desc p) {
+  const int segs = (p.w + 511) >> 9;
+  const long long hw = (long long)p.h * p.w;
+  const int waves = p.n * p.h * segs;
+  const int lane = threadIdx.x & 63;
+  constexpr unsigned kOut = 0x80000000u;
+  for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
+       wv += gridDim.x * 4) {
+    const int sg = wv % segs;
+    const int r = wv / segs;
+    const int y = r % p.h, n = r / p.h;
+    const __amdgpu_buffer_rsrc_t rf0 = warp_plane(p.flow + (long long)n * 2 * hw, hw);
+    const __amdgpu_buffer_rsrc_t rf1 = warp_plane(p.flow + ((long long)n * 2 + 1) * hw, hw);
+    float fx[4][2], fy[4][2];
+    bool live[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = (sg << 9) + 2 * lane + 128 * k;
+      live[k] = x < p.w;  // (even width: the pair is live or dead as a whole)
+      const unsigned fo = (unsigned)(y * p.w + (live[k] ? x : p.w - 2)) * 4u;
+      const auto a = __builtin_amdgcn_raw_buffer_load_b64(rf0, fo, 0, 0);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b64(rf1, fo, 0, 0);
+      fx[k][0] = __uint_as_float(a[0]);
+      fx[k][1] = __uint_as_float(a[1]);
+      fy[k][0] = __uint_as_float(b[0]);
+      fy[k][1] = __uint_as_float(b[1]);
+    }
+    WarpTap t[4][2];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = live[k] ? (sg << 9) + 2 * lane + 128 * k : p.w - 2;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) t[k][e] = warp_tap(x + e, y, fx[k][e], fy[k][e], p.w, p.h, p.align_corners);
+      const int dx = t[k][1].x0 - t[k][0].x0;
+      ok = ok && t[k][1].y0 == t[k][0].y0 && dx >= 0 && dx <= 2 && t[k][0].x0 >= 0 && t[k][0].x0 + 3 < p.w;
+    }
+    const bool fast = __all(ok);
+    auto store = [&](int c, const float (*o)[2]) {
+      const __amdgpu_buffer_rsrc_t out = warp_plane(p.out + ((long long)n * CC + c) * hw, hw);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // dead pairs: out-of-range offset, store dropped
+        const unsigned off = live[k] ? (unsigned)(y * p.w + (sg << 9) + 2 * lane + 128 * k) * 4u : kOut;
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, (f32x2_t{o[k][0], o[k][1]})), out, off, 0, 0);
+      }
+    };
+    if (fast) {
+      i32x4 u[CC][4], v[CC][4];
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + ((long long)n * CC + c) * hw, hw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const WarpTap& t0 = t[k][0];
+          const unsigned r0 = (unsigned)(t0.y0 * p.w + t0.x0), r1 = (unsigned)((t0.y0 + 1) * p.w + t0.x0);
+          u[c][k] = __builtin_amdgcn_raw_buffer_load_b128(im, t0.vy0 ? r0 * 4u : kOut, 0, 0);
+          v[c][k] = __builtin_amdgcn_raw_buffer_load_b128(im, t0.vy1 ? r1 * 4u : kOut, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        float o[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int dx = t[k][1].x0 - t[k][0].x0;
+          const i32x4 uu = u[c][k], vv = v[c][k];
+          o[k][0] = warp_blend(__int_as_float(uu[0]), __int_as_float(uu[1]), __int_as_float(vv[0]),
+                               __int_as_float(vv[1]), t[k][0]);
+          const int ua = dx == 0 ? uu[0] : dx == 1 ? uu[1] : uu[2];
+          const int ub = dx == 0 ? uu[1] : dx == 1 ? uu[2] : uu[3];
+          const int va = dx == 0 ? vv[0] : dx == 1 ? vv[1] : vv[2];
+          const int vb = dx == 0 ? vv[1] : dx == 1 ? vv[2] : vv[3];
+          o[k][1] = warp_blend(__int_as_float(ua), __int_as_float(ub), __int_as_float(va), __int_as_float(vb), t[k][1]);
+        }
+        store(c, o);
+      }
+    } else {
+      float vv[CC][4][2][4];
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + ((long long)n * CC + c) * hw, hw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            warp_corners(im, t[k][e], p.w, vv[c][k][e][0], vv[c][k][e][1], vv[c][k][e][2], vv[c][k][e][3]);
+      }
+#pragma unroll
+      for (int c = 0; c < CC; ++c) {
+        float o[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            o[k][e] = warp_blend(vv[c][k][e][0], vv[c][k][e][1], vv[c][k][e][2], vv[c][k][e][3], t[k][e]);
         store(c, o);
       }
     }
@@ -514,6 +627,9 @@ __global__ void scale_kernel(float* p, long long n, float s) {
     p[i] *= s;
 }
 
+// DVIE_WARP_FWD2=0: the one-pixel-per-lane forward (A/B runs); read once
+static const bool warp_fwd2_on = !(getenv("DVIE_WARP_FWD2") && *getenv("DVIE_WARP_FWD2") == '0');
+
 static int grid_for(long long n) {
   long long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -532,7 +648,10 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
   DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
   const int grid = grid_for(waves * 256);
-  if (d->c == 3)
+  if (d->c == 3 && d->w % 2 == 0 && d->w >= 4 && warp_fwd2_on) {
+    const long long waves2 = (long long)d->n * d->h * ((d->w + 511) / 512);
+    hipLaunchKernelGGL(warp_fwd2_kernel<3>, dim3(grid_for(waves2 * 256)), dim3(256), 0, (hipStream_t)stream, *d);
+  } else if (d->c == 3)
     hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
   else
     hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
@@ -617,19 +736,17 @@ int dvie_scale(float* p, long long n, float s, void* stream) {
 }  // extern "C"
 
 // Lanes of the op-list executor (dvie_op.lane, include/dvie.h): lane 0 is the caller's
-// stream; lanes 1..7 are side streams of the current device and host thread, created on
-// first use at the default (lowest) priority, as the caller's stream.  Events are re-recorded at every use:
-// a stream wait binds to the record that precedes it.
+// stream; lane 1 (the weight lane) is a side stream of the current device and host thread,
+// created on first use at the default (lowest) priority, as the caller's stream.  Events
+// are re-recorded at every use: a stream wait binds to the record that precedes it.
 namespace {
-constexpr int kLanes = 8;
 struct DevLanes {
-  hipStream_t s[kLanes] = {};
-  hipEvent_t join[kLanes] = {};
-  hipEvent_t fork = nullptr, tail = nullptr;
+  hipStream_t side = nullptr;
+  hipEvent_t join = nullptr, tail = nullptr;
   bool ok = false;
 };
 // per host thread (the forward and the autograd backward thread each get their own side
-// streams and events, so calls from two threads never re-record each other's events)
+// stream and events, so calls from two threads never re-record each other's events)
 thread_local DevLanes dev_lanes[64];
 
 DevLanes* lanes_of_device() {
@@ -639,12 +756,8 @@ DevLanes* lanes_of_device() {
   if (!d.ok) {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-    for (int l = 1; l < kLanes; ++l) {
-      if (hipStreamCreateWithPriority(&d.s[l], hipStreamNonBlocking, least) != hipSuccess ||
-          hipEventCreateWithFlags(&d.join[l], hipEventDisableTiming) != hipSuccess)
-        return nullptr;
-    }
-    if (hipEventCreateWithFlags(&d.fork, hipEventDisableTiming) != hipSuccess ||
+    if (hipStreamCreateWithPriority(&d.side, hipStreamNonBlocking, least) != hipSuccess ||
+        hipEventCreateWithFlags(&d.join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&d.tail, hipEventDisableTiming) != hipSuccess)
       return nullptr;
     d.ok = true;
@@ -657,70 +770,28 @@ bool lanes_on() {
   return !(e && *e == '0');
 }
 
-// per-call lane bookkeeping
+// per-call lane bookkeeping: every data op runs on the caller's stream, so a weight-lane op
+// that follows any data op waits for the caller's stream at its current position
 struct LaneRun {
   DevLanes* d = nullptr;
   hipStream_t main = nullptr;
-  int data_lane = 0;          // lane of the last non-weight-lane op
-  bool tail_fresh = false;    // lane 1 already waits for the data lane's current position
-  bool fork_valid = false;    // d->fork holds this call's current fork point
-  bool waited[kLanes] = {};   // branch lane waits on the current fork point
-  bool in_region[kLanes] = {};
-  bool used[kLanes] = {};
+  bool tail_fresh = false;  // the weight lane already waits for the caller's current position
+  bool used = false;
 
-  hipStream_t st(int l) const { return l == 0 ? main : d->s[l]; }
-
-  hipError_t join_lane(int l) {
-    hipError_t e = hipEventRecord(d->join[l], d->s[l]);
-    return e == hipSuccess ? hipStreamWaitEvent(main, d->join[l], 0) : e;
-  }
-  // FORK: the branch lanes' next ops wait for everything issued on the caller's stream so far
-  hipError_t fork() {
-    for (int l = 2; l < kLanes; ++l) waited[l] = false;
-    fork_valid = true;
-    data_lane = 0;
-    return hipEventRecord(d->fork, main);
-  }
-  // JOIN: the caller's stream waits for the branch lanes used since the fork
-  hipError_t join_region() {
+  hipError_t enter_weight() {
     hipError_t e = hipSuccess;
-    for (int l = 2; l < kLanes && e == hipSuccess; ++l)
-      if (in_region[l]) {
-        e = join_lane(l);
-        in_region[l] = false;
-      }
-    data_lane = 0;
-    tail_fresh = false;
-    return e;
-  }
-  // stream for an op of lane l (waits inserted as needed)
-  hipError_t enter(int l, hipStream_t* out) {
-    hipError_t e = hipSuccess;
-    if (l == 1) {
-      if (!tail_fresh) {  // the weight lane follows the data lane that produced its inputs
-        e = hipEventRecord(d->tail, st(data_lane));
-        if (e == hipSuccess) e = hipStreamWaitEvent(d->s[1], d->tail, 0);
-        tail_fresh = true;
-      }
-    } else {
-      if (l >= 2 && !waited[l]) {
-        if (!fork_valid) e = fork();  // branch ops without a FORK in this call: fork here
-        if (e == hipSuccess) e = hipStreamWaitEvent(d->s[l], d->fork, 0);
-        waited[l] = true;
-      }
-      if (l >= 2) in_region[l] = true;
-      data_lane = l;
-      tail_fresh = false;
+    if (!tail_fresh) {
+      e = hipEventRecord(d->tail, main);
+      if (e == hipSuccess) e = hipStreamWaitEvent(d->side, d->tail, 0);
+      tail_fresh = true;
     }
-    used[l] = true;
-    *out = st(l);
+    used = true;
     return e;
   }
   hipError_t finish() {
-    hipError_t e = hipSuccess;
-    for (int l = 1; l < kLanes && e == hipSuccess; ++l)
-      if (used[l]) e = join_lane(l);
-    return e;
+    if (!used) return hipSuccess;
+    hipError_t e = hipEventRecord(d->join, d->side);
+    return e == hipSuccess ? hipStreamWaitEvent(main, d->join, 0) : e;
   }
 };
 }  // namespace
@@ -744,37 +815,25 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
   for (int i = 0; i < n; ++i) {
     int rc = DVIE_OK;
     const dvie_op& o = ops[i];
-    if (o.lane < 0 || o.lane >= kLanes) {
+    if (o.lane < 0 || o.lane > 1) {
       set_error("run_ops: lane %d of op %d out of range", o.lane, i);
       return finish(DVIE_EINVAL);
     }
-    const bool marker = o.kind == DVIE_OP_FORK || o.kind == DVIE_OP_JOIN;
     hipStream_t st = lr.main;
-    if (lanes && (o.lane != 0 || marker)) {
+    if (lanes && o.lane == 1) {
       if (!lr.d) lr.d = lanes_of_device();
       if (!lr.d) {
-        set_error("run_ops: side streams unavailable");
+        set_error("run_ops: side stream unavailable");
         return finish(DVIE_EINVAL);
       }
-      hipError_t e = hipSuccess;
-      if (o.kind == DVIE_OP_FORK)
-        e = lr.fork();
-      else if (o.kind == DVIE_OP_JOIN)
-        e = lr.join_region();
-      else
-        e = lr.enter(o.lane, &st);
-      if (e != hipSuccess) {
-        set_error("run_ops: lane fork / join failed at op %d", i);
-        return finish((int)e);
+      if (lr.enter_weight() != hipSuccess) {
+        set_error("run_ops: weight-lane wait failed at op %d", i);
+        return finish(DVIE_EINVAL);
       }
-    } else if (lr.d && !marker) {
-      const hipError_t e = lr.enter(0, &st);
-      if (e != hipSuccess) {
-        set_error("run_ops: lane 0 entry failed at op %d", i);
-        return finish((int)e);
-      }
+      st = lr.d->side;
+    } else {
+      lr.tail_fresh = false;  // the caller's stream moves on past the weight lane's wait
     }
-    if (marker) continue;
     void* s = (void*)st;
     switch (o.kind) {
       case DVIE_OP_CONV: rc = dvie_conv2d_fwd(&o.u.conv, s); break;
@@ -789,6 +848,8 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
       case DVIE_OP_HEAD_FWD: rc = dvie_head_fwd(&o.u.head, s); break;
       case DVIE_OP_HEAD_BWD: rc = dvie_head_bwd(&o.u.head, s); break;
       case DVIE_OP_ATTN: rc = dvie_attn(&o.u.attn, s); break;
+      case DVIE_OP_HEAD3_BWD: rc = dvie_head3_bwd(&o.u.head3, s); break;
+      case DVIE_OP_SEGENC_FWD: rc = dvie_segenc_fwd(&o.u.segenc, s); break;
       default: set_error("run_ops: unknown op kind %d at %d", o.kind, i); return finish(DVIE_EINVAL);
     }
     if (rc != DVIE_OK) {
@@ -817,6 +878,8 @@ size_t dvie_abi_sizeof(int which) {
     case DVIE_OP_BN_FWD: return sizeof(dvie_bn_desc);
     case DVIE_OP_HEAD_FWD: return sizeof(dvie_head_desc);
     case DVIE_OP_ATTN: return sizeof(dvie_attn_desc);
+    case DVIE_OP_HEAD3_BWD: return sizeof(dvie_head3_bwd_desc);
+    case DVIE_OP_SEGENC_FWD: return sizeof(dvie_segenc_desc);
     case 100: return sizeof(dvie_warp_desc);
     case 101: return sizeof(dvie_softmax_desc);
     case 102: return sizeof(dvie_sn_layer);

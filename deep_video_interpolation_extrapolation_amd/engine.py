@@ -18,7 +18,6 @@ Each list runs with a single host call (`dvie_run_ops`) on the current HIP strea
 All activations are NHWC buffers allocated once per (batch, height, width) plan; the
 kernels never allocate.  Reference semantics: nets/HRNet.py, nets/vgg.py, losses.py.
 """
-import contextlib
 import ctypes
 import math
 import os
@@ -179,27 +178,7 @@ class ConvLayer:
 
 
 class _Op:
-    lane = 0  # executor lane (dvie_op.lane): 0 the caller's stream, 2.. branch lanes
-
-
-class ForkOp(_Op):
-    """Start of a branch region: ops of different lanes until the matching JoinOp are
-    independent (no op of one lane reads a buffer another lane's op writes) and run on their
-    own streams (DVIE_OP_FORK / DVIE_OP_JOIN, include/dvie.h).  backward=True: the backward
-    mirrors the region (valid when every gradient the region's ops emit stays in the lane
-    that produced its inputs); False: the backward of its ops runs on lane 0."""
-    out = None
-    act = 0
-
-    def __init__(self, backward=True):
-        self.backward = backward
-
-    def inputs(self):
-        return []
-
-
-class JoinOp(ForkOp):
-    """End of a branch region."""
+    pass
 
 
 class ConvOp(_Op):
@@ -415,7 +394,6 @@ class Graph:
         self.layers = []
         self.outputs = {}
         self.n_l1 = 0
-        self.cur_lane = 0
 
     # ---------------- builder ----------------
     def buffer(self, name, H, W, C, dtype=None, external=False):
@@ -548,28 +526,13 @@ class Graph:
     def output(self, key, region, channels):
         self.outputs[key] = (region, channels)
 
-    # ---- branch regions (independent lanes; see ForkOp) ----
-    def fork(self, backward=True):
-        self._region = ForkOp(backward)
-        self._add(self._region)
-
-    def join(self):
-        self._add(JoinOp(self._region.backward))
-        self._region = None
-
-    @contextlib.contextmanager
-    def lane(self, k):
-        prev, self.cur_lane = self.cur_lane, k
-        try:
-            yield
-        finally:
-            self.cur_lane = prev
+    def segenc_chain(self, ops):
+        """mark three ConvOps as HRNet's segmentation encoder (conv + ELU, conv + ELU, conv):
+        the plan runs their forward as one dvie_segenc_fwd launch where the shapes allow
+        (Plan._segenc_fwd); their backward is unchanged."""
+        self.__dict__.setdefault("segenc", []).append(tuple(ops))
 
     def _add(self, op):
-        if not isinstance(op, ForkOp):
-            op.lane = self.cur_lane
-            reg = getattr(self, "_region", None)
-            op.bwd_lane = op.lane if reg is None or reg.backward else 0
         self.ops.append(op)
         if op.out is not None:
             op.out.buf.producers.append(op)
@@ -579,23 +542,6 @@ class Graph:
     # ---------------- compile ----------------
     def compile(self, n_fwd, device, n_bwd=None, backward=True):
         return Plan(self, n_fwd, n_fwd if n_bwd is None else n_bwd, device, backward)
-
-
-class _Ops(list):
-    """A plan's descriptor list: every appended descriptor takes the lane of the graph op
-    being lowered (Plan.cur_lane)."""
-
-    def __init__(self, plan):
-        super().__init__()
-        self.plan = plan
-
-    def append(self, o):
-        o.lane = self.plan.cur_lane
-        super().append(o)
-
-    def extend(self, ops):
-        for o in ops:
-            self.append(o)
 
 
 class Plan:
@@ -612,9 +558,8 @@ class Plan:
         self.busy = False
         self.generation = 0
         self._alloc()
-        self.cur_lane = 0  # lane of the graph op whose descriptors are being emitted
-        self.fwd = _Ops(self)
-        self.bwd = _Ops(self)
+        self.fwd = []
+        self.bwd = []
         self._l1_fwd = []  # (forward list index, level) of the VGG feature-L1 loss ops
         self.ext_in = {}  # key -> list of (op index, InputOp) for patching
         self.ext_out = {}
@@ -805,13 +750,55 @@ class Plan:
         return (0 if part == 0 else self.nf // 2), self.nf // 2
 
     # ---------------- forward ----------------
+    def _segenc_fusable(self, ops):
+        if self.dtype != torch.bfloat16 or os.environ.get("DVIE_SEGENC_FUSED", "1") == "0":
+            return False
+        o0, o1, o2 = ops
+        acts = (L.ACT_ELU, L.ACT_ELU, L.ACT_NONE)
+        chans = ((24, 32), (32, 32), (32, 8))
+        for op, act, (ci, co) in zip(ops, acts, chans):
+            lay = op.layer
+            if not (isinstance(op, ConvOp) and op.act == act and op.res is None and lay.kh == 3 and lay.kw == 3
+                    and lay.stride == 1 and lay.pad == 1 and lay.dil == 1 and lay.has_bias and op.x.c == ci
+                    and op.out.c == co and lay.cout_p == co):
+                return False
+        if not (o1.x.buf is o0.out.buf and o2.x.buf is o1.out.buf and o0.out.c0 == 0 and o1.out.c0 == 0):
+            return False
+        if o0.out.buf.C != 32 or o1.out.buf.C != 32 or o2.out.buf.external:
+            return False
+        x = o0.x
+        return self.nf * x.H * x.W * x.buf.C * 2 < 0xFFFFFF00
+
+    def _segenc_fwd(self, ops):
+        o0, o1, o2 = ops
+        x, nf = o0.x, self.nf
+        o = self._op(L.OP_SEGENC_FWD)
+        d = o.u.segenc
+        d.inp, d.e1, d.e2, d.out = self.ptr(x), self.ptr(o0.out), self.ptr(o1.out), self.ptr(o2.out)
+        d.in_ld, d.e1_ld, d.e2_ld, d.out_ld = x.buf.C, o0.out.buf.C, o1.out.buf.C, o2.out.buf.C
+        d.w0, d.w2, d.w4 = o0.layer.wf.data_ptr(), o1.layer.wf.data_ptr(), o2.layer.wf.data_ptr()
+        d.b0, d.b2, d.b4 = o0.layer.bias_p.data_ptr(), o1.layer.bias_p.data_ptr(), o2.layer.bias_p.data_ptr()
+        d.n, d.h, d.w = nf, x.H, x.W
+        d.kpad0, d.kpad2, d.kpad4 = o0.layer.kpad, o1.layer.kpad, o2.layer.kpad
+        npx = nf * x.H * x.W
+        o.meta = dict(cls="conv_fwd", name="seg_encoder (fused)",
+                      flops=2.0 * npx * 9 * sum(op.layer.cout * op.layer.cin for op in ops),
+                      bytes=float(self.es * npx * (x.c + 32 + 32 + 8)))
+        return o
+
     def _build_forward(self):
         g = self.g
         nf = self.nf
+        fused_first, skip = {}, set()
+        for chain in getattr(g, "segenc", []):
+            if self._segenc_fusable(chain):
+                fused_first[id(chain[0])] = chain
+                skip.update(id(op) for op in chain[1:])
         for op in g.ops:
-            self.cur_lane = op.lane
-            if isinstance(op, ForkOp):  # (JoinOp included)
-                self.fwd.append(self._op(L.OP_JOIN if isinstance(op, JoinOp) else L.OP_FORK))
+            if id(op) in skip:
+                continue
+            if id(op) in fused_first:
+                self.fwd.append(self._segenc_fwd(fused_first[id(op)]))
                 continue
             if isinstance(op, InputOp):
                 n0, cnt = self._part(op.part)
@@ -914,7 +901,7 @@ class Plan:
                 d.a_sn, d.a_sc, d.a_sh, d.a_sw = sn, 1, sh, sw
                 d.b_sn, d.b_sc, d.b_sh, d.b_sw = sn, 1, sh, sw
                 d.kind, d.bsz, d.ch, d.h, d.w, d.dtype = L.LOSS_L1NHWC, half, a.c, a.H, a.W, self.dt
-                d.weight = 1.0
+                d.weight, d.out_scale = 1.0, 1.0
                 npart = L.load().dvie_loss_partial_count(ctypes.byref(d))
                 part = torch.zeros(max(1, npart), dtype=torch.float64, device=self.device)
                 self.keep.append(part)
@@ -1050,12 +1037,7 @@ class Plan:
         pend = b.pending.setdefault(key, [])
         pend.append((emitter, ident))
         if len(pend) == b.expected[key]:
-            if self._region_open and id(b) in self._shared_in:
-                # read by several lanes of the region being mirrored: its contributions come
-                # from different lanes, so it is summed on lane 0 after the region's JOIN
-                self._deferred.append((b, key))
-            else:
-                self._flush(b, key)
+            self._flush(b, key)
 
     def _flush(self, b, key):
         c0, c = key
@@ -1112,28 +1094,9 @@ class Plan:
         self.bwd.append(self.ew_desc(L.EW_COPY, self.nb, out.H, out.W, out.c, gp, b.C, [(gp, b.C, out.H, out.W)],
                                      z=self.ptr(out), z_ld=b.C, dact=op.act))
 
-    def _shared_region_inputs(self):
-        """ids of the buffers that ops of more than one lane read inside a backward-mirrored
-        branch region (their gradients sum contributions from several lanes)."""
-        shared, lanes = set(), None
-        for op in self.g.ops:
-            if isinstance(op, JoinOp):
-                shared.update(k for k, ls in lanes.items() if len(ls) > 1)
-                lanes = None
-            elif isinstance(op, ForkOp):
-                lanes = {} if op.backward else None
-            elif lanes is not None:
-                for r in op.inputs():
-                    lanes.setdefault(id(r.buf), set()).add(op.lane)
-        return shared
-
     def _build_backward(self):
         g = self.g
         nb = self.nb
-        self.cur_lane = 0
-        self._shared_in = self._shared_region_inputs()
-        self._region_open = False
-        self._deferred = []
         self.wg_first = {}
         self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
         self._uses_left = {}
@@ -1151,17 +1114,6 @@ class Plan:
             b.done = True
             b.dact_done = all(p.act == L.ACT_NONE for p in b.producers)  # else _ensure_dact at the producer
         for op in reversed(g.ops):
-            self.cur_lane = getattr(op, "bwd_lane", 0)
-            if isinstance(op, ForkOp):  # the backward runs the region the other way round
-                if op.backward:
-                    opening = isinstance(op, JoinOp)
-                    self.bwd.append(self._op(L.OP_FORK if opening else L.OP_JOIN))
-                    self._region_open = opening
-                    if not opening:  # every lane joined: the shared inputs' gradients
-                        for b, key in self._deferred:
-                            self._flush(b, key)
-                        self._deferred = []
-                continue
             if isinstance(op, OutNCHWOp):
                 continue
             if isinstance(op, HeadOp):
@@ -1286,67 +1238,87 @@ class Plan:
                 raise RuntimeError(f"incomplete gradient for {bf}: pending {({k: len(v) for k, v in bf.pending.items()})}"
                                    f" of {bf.expected}")
 
+    def _head3_fusable(self, op, gld):
+        """Narrow-output 3x3 head conv (HRNet rgb_layer[2] / seg_layer[2]) whose backward can
+        run as one dvie_head3_bwd pass over its input (DVIE_HEAD3_FUSED=0: unfused)."""
+        lay, x, out = op.layer, op.x, op.out
+        if self.dtype != torch.bfloat16 or os.environ.get("DVIE_HEAD3_FUSED", "1") == "0":
+            return False
+        if not (lay.trainable and x.buf.needs_grad and op.res is None and lay.kh == 3 and lay.kw == 3
+                and lay.stride == 1 and lay.pad == 1 and lay.dil == 1 and lay.cout_p in (8, 24)
+                and x.c % 64 == 0 and (out.H, out.W) == (x.H, x.W)):
+            return False
+        if x.buf.expected.get(x.key(), 0) != 1 or lay.cmap_t is not None and lay.cin != x.c:
+            return False
+        npx = self.nb * x.H * x.W
+        return npx * max(x.buf.C, gld) * 2 < 0xFFFFFF00
+
+    def _head3_ops(self, op, gout, gld, phase, xg, dact):
+        """dvie_head3_bwd (data gradient with act' + weight-gradient slabs in one pass over
+        the input) into its own slab buffer, then on the weight lane the bias column sums and
+        the slab reductions; the weight-gradient bookkeeping of _emit_wgrad."""
+        lay, x, out = op.layer, op.x, op.out
+        nb = self.nb
+        ph, wt, kpad = phase
+        n_cb = x.c // 64
+        splits = max(1, 256 // n_cb)
+        slabs = torch.empty(splits * lay.cout_p * 9 * x.c, dtype=torch.float32, device=self.device)
+        self.keep.append(slabs)
+        o = self._op(L.OP_HEAD3_BWD)
+        d = o.u.head3
+        d.g, d.h, d.wd, d.dh, d.ws = gout, self.ptr(x), wt.data_ptr(), xg, slabs.data_ptr()
+        d.g_ld, d.h_ld, d.dh_ld = gld, x.buf.C, x.buf.C
+        d.n, d.hgt, d.wid, d.c = nb, x.H, x.W, x.c
+        d.cout, d.kpad, d.dy0, d.dx0 = lay.cout_p, kpad, ph["dy0"], ph["dx0"]
+        d.splits, d.dact, d.alpha = splits, dact, 0.2
+        npix = nb * x.H * x.W
+        o.meta = dict(cls="conv_dgrad", name=lay.name + "+wgrad",
+                      flops=2.0 * npix * lay.cout * lay.cin * 9 * 2,
+                      bytes=float(self.es * (2 * npix * x.c + npix * lay.cout) + 4 * slabs.numel()))
+        ops = [o]
+        first = lay not in self.wg_first
+        base = len(self.bwd)
+        if lay.has_bias:
+            csplits = max(1, min(2048, npix // 512))
+            c = self._op(L.OP_COLSUM)
+            cd = c.u.colsum
+            cd.g, cd.ws, cd.g_ld, cd.rows, cd.c, cd.splits, cd.dtype = gout, 0, gld, npix, lay.cout_p, csplits, self.dt
+            self.ws_floats = max(self.ws_floats, csplits * lay.cout_p)
+            ops.append(c)
+        r_op = self._op(L.OP_WREDUCE)
+        r = r_op.u.wreduce
+        r.ws, r.dw, r.cmap = slabs.data_ptr(), 0, lay.cmap_t.data_ptr()
+        r.splits, r.ws_rows, r.ws_k, r.co_off = splits, lay.cout_p, 9 * x.c, 0
+        r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
+        r.beta = 0 if first else 1
+        r_op.ws_ptr = slabs.data_ptr()
+        r_op.meta = _reduce_meta(lay.name, r)
+        ops.append(r_op)
+        self._grad_slots.append((base + len(ops) - 1, lay, "weight", first))
+        if lay.has_bias:
+            b_op = self._op(L.OP_WREDUCE)
+            r = b_op.u.wreduce
+            r.ws, r.dw, r.cmap = 0, 0, None
+            r.splits, r.ws_rows, r.ws_k, r.co_off = csplits, lay.cout_p, 1, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
+            r.beta = 0 if first else 1
+            b_op.meta = _reduce_meta(lay.name + ".bias", r)
+            ops.append(b_op)
+            self._grad_slots.append((base + len(ops) - 1, lay, "bias", first))
+        self.wg_first[lay] = True
+        self._uses_left[lay] -= 1
+        if self._uses_left[lay] == 0:
+            self.completions.append((base + len(ops), lay))
+        return ops
+
     def _conv_backward(self, op, gout, gld):
         lay, x, out = op.layer, op.x, op.out
         nb = self.nb
         npix = nb * out.H * out.W
         taps = lay.fwd_taps()
-        if lay.trainable:
-            # weight gradient: split-K partial slabs + reduction into the OIHW .grad view
-            tiles = rup(lay.cout_p, 64) // 64 * (rup(x.c, 64) // 64)
-            ntap = lay.kh * lay.kw
-            bkp = 64 if self.dtype == torch.bfloat16 else 32
-            splits = max(1, min(max(1, npix // (bkp * 4)), 1024 // max(1, tiles * ntap)))
-            o = self._op(L.OP_WGRAD)
-            d = o.u.wgrad
-            d.g, d.x, d.ws = gout, self.ptr(x), 0
-            d.g_ld, d.x_ld = gld, x.buf.C
-            d.n, d.oh, d.ow, d.cout = nb, out.H, out.W, lay.cout_p
-            d.ih, d.iw, d.c, d.sy, d.sx = x.H, x.W, x.c, lay.stride, lay.stride
-            d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], taps["ddy"], \
-                taps["ddx"]
-            d.dtype = self.dt
-            lib = L.load()
-            hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))  # the halo kernel's preferred split
-            d.splits = hint if hint > 0 else splits
-            slabs = lib.dvie_wgrad_slabs(ctypes.byref(d))
-            wfl = slabs * lay.cout_p * ntap * x.c
-            bslabs = 0
-            if lay.has_bias:  # bias column sums ride on the weight-gradient launch (d.bws)
-                d.bws = 1  # placeholder (set in _finalize): makes the query see a bias launch
-                bslabs = lib.dvie_wgrad_bias_slabs(ctypes.byref(d))
-                d.bws = None
-                o.bws_off = wfl
-            self.ws_floats = max(self.ws_floats, wfl + bslabs * lay.cout_p)
-            o.meta = dict(cls="conv_wgrad", name=lay.name, flops=2.0 * npix * lay.cout * lay.cin * ntap,
-                          bytes=float(self.es * (npix * lay.cout + nb * x.H * x.W * lay.cin)
-                                      + 4 * slabs * lay.cout_p * ntap * x.c))
-            self.bwd.append(o)
-            o = self._op(L.OP_WREDUCE)
-            r = o.u.wreduce
-            r.ws, r.dw, r.cmap = 0, 0, lay.cmap_t.data_ptr()
-            r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, ntap * x.c, 0
-            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
-            first = lay not in self.wg_first
-            r.beta = 0 if first else 1
-            o.meta = _reduce_meta(lay.name, r)
-            self.bwd.append(o)
-            self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
-            if lay.has_bias:
-                o = self._op(L.OP_WREDUCE)
-                r = o.u.wreduce
-                r.ws, r.dw, r.cmap = 0, 0, None
-                r.splits, r.ws_rows, r.ws_k, r.co_off = bslabs, lay.cout_p, 1, 0
-                r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
-                r.beta = 0 if first else 1
-                o.meta = _reduce_meta(lay.name + ".bias", r)
-                o.ws_off = wfl
-                self.bwd.append(o)
-                self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
-            self.wg_first[lay] = True
-            self._uses_left[lay] -= 1
-            if self._uses_left[lay] == 0:
-                self.completions.append((len(self.bwd), lay))
+        head3 = self._head3_fusable(op, gld)
+        if lay.trainable and not head3:
+            self._emit_wgrad(op, gout, gld)
         if op.res is not None and op.res.buf.needs_grad:
             self._contrib(op.res, None, ident=(gout, gld))
         if x.buf.needs_grad:
@@ -1354,6 +1326,11 @@ class Plan:
             xg = self.ptr(x, grad=True)
 
             def em(beta, res, res_ld, dact, z, z_ld, phases=phases, x=x, xg=xg, out=out, gout=gout, gld=gld, lay=lay):
+                if head3:
+                    if beta == 0 and res is None and dact in (L.ACT_NONE, L.ACT_LRELU) and \
+                            (z is None or z == self.ptr(x)) and len(phases) == 1:
+                        return self._head3_ops(op, gout, gld, phases[0], xg, dact)
+                    self._emit_wgrad(op, gout, gld)  # (not the expected pattern: unfused)
                 ops = []
                 if self._im2col_dgrad(lay, x, phases):
                     return self._im2col_dgrad_ops(lay, x, xg, out, gout, gld, phases[0], res, res_ld, z, z_ld, dact,
@@ -1375,6 +1352,69 @@ class Plan:
 
             self._contrib(x, em)
 
+    def _emit_wgrad(self, op, gout, gld):
+        """weight (and bias) gradient of a conv: split-K partial slabs + reduction into the
+        OIHW .grad view, appended to the backward list (weight lane)."""
+        lay, x, out = op.layer, op.x, op.out
+        nb = self.nb
+        npix = nb * out.H * out.W
+        taps = lay.fwd_taps()
+        # weight gradient: split-K partial slabs + reduction into the OIHW .grad view
+        tiles = rup(lay.cout_p, 64) // 64 * (rup(x.c, 64) // 64)
+        ntap = lay.kh * lay.kw
+        bkp = 64 if self.dtype == torch.bfloat16 else 32
+        splits = max(1, min(max(1, npix // (bkp * 4)), 1024 // max(1, tiles * ntap)))
+        o = self._op(L.OP_WGRAD)
+        d = o.u.wgrad
+        d.g, d.x, d.ws = gout, self.ptr(x), 0
+        d.g_ld, d.x_ld = gld, x.buf.C
+        d.n, d.oh, d.ow, d.cout = nb, out.H, out.W, lay.cout_p
+        d.ih, d.iw, d.c, d.sy, d.sx = x.H, x.W, x.c, lay.stride, lay.stride
+        d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = taps["th"], taps["tw"], taps["dy0"], taps["dx0"], taps["ddy"], \
+            taps["ddx"]
+        d.dtype = self.dt
+        lib = L.load()
+        hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))  # the halo kernel's preferred split
+        d.splits = hint if hint > 0 else splits
+        slabs = lib.dvie_wgrad_slabs(ctypes.byref(d))
+        wfl = slabs * lay.cout_p * ntap * x.c
+        bslabs = 0
+        if lay.has_bias:  # bias column sums ride on the weight-gradient launch (d.bws)
+            d.bws = 1  # placeholder (set in _finalize): makes the query see a bias launch
+            bslabs = lib.dvie_wgrad_bias_slabs(ctypes.byref(d))
+            d.bws = None
+            o.bws_off = wfl
+        self.ws_floats = max(self.ws_floats, wfl + bslabs * lay.cout_p)
+        o.meta = dict(cls="conv_wgrad", name=lay.name, flops=2.0 * npix * lay.cout * lay.cin * ntap,
+                      bytes=float(self.es * (npix * lay.cout + nb * x.H * x.W * lay.cin)
+                                  + 4 * slabs * lay.cout_p * ntap * x.c))
+        self.bwd.append(o)
+        o = self._op(L.OP_WREDUCE)
+        r = o.u.wreduce
+        r.ws, r.dw, r.cmap = 0, 0, lay.cmap_t.data_ptr()
+        r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, ntap * x.c, 0
+        r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, x.c
+        first = lay not in self.wg_first
+        r.beta = 0 if first else 1
+        o.meta = _reduce_meta(lay.name, r)
+        self.bwd.append(o)
+        self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
+        if lay.has_bias:
+            o = self._op(L.OP_WREDUCE)
+            r = o.u.wreduce
+            r.ws, r.dw, r.cmap = 0, 0, None
+            r.splits, r.ws_rows, r.ws_k, r.co_off = bslabs, lay.cout_p, 1, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
+            r.beta = 0 if first else 1
+            o.meta = _reduce_meta(lay.name + ".bias", r)
+            o.ws_off = wfl
+            self.bwd.append(o)
+            self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
+        self.wg_first[lay] = True
+        self._uses_left[lay] -= 1
+        if self._uses_left[lay] == 0:
+            self.completions.append((len(self.bwd), lay))
+
     def _im2col_dgrad(self, lay, x, phases):
         """Narrow-input stride-1 data gradients (HRNet's 3x3 448->3 / 448->20 heads: the
         output gradient has 8 / 24 channels) run as im2col + 1x1 GEMM over K = 9*c (128 /
@@ -1395,13 +1435,11 @@ class Plan:
         ph, wt, kpad = phase
         nb = self.nb
         npx = nb * ph["oh"] * ph["ow"]
-        # one scratch per executor lane, shared by the layers of that lane (in order on its
-        # stream): the two heads' data gradients run on different lanes
-        scratch = self.__dict__.setdefault("_i2c", {})
-        buf = scratch.get(self.cur_lane)
+        # one scratch shared by the layers (in order on the data lane)
+        buf = self.__dict__.get("_i2c")
         if buf is None or buf.numel() < npx * kpad:
             buf = torch.empty(npx * kpad, dtype=self.dtype, device=self.device)
-            scratch[self.cur_lane] = buf
+            self._i2c = buf
             self.keep.append(buf)
         e = self.ew_desc(L.EW_IM2COL, nb, out.H, out.W, kpad, buf.data_ptr(), kpad,
                          srcs=[(gout, gld, ph["th"], ph["tw"]), (None, 0, ph["dy0"], ph["dx0"]),
@@ -1513,7 +1551,7 @@ class Plan:
             elif o.kind == L.OP_COLSUM:
                 o.u.colsum.ws = self.ws.data_ptr()
             elif o.kind == L.OP_WREDUCE:
-                o.u.wreduce.ws = self.ws.data_ptr() + 4 * getattr(o, "ws_off", 0)
+                o.u.wreduce.ws = getattr(o, "ws_ptr", None) or self.ws.data_ptr() + 4 * getattr(o, "ws_off", 0)
         # pack op (all layers, one launch) goes first in the forward list
         descs = self._pack_descs
         if not descs:  # no convolutions (e.g. a pointwise-only plan)
@@ -1682,6 +1720,19 @@ class Plan:
                 out[b.name] = (b.t > 0).permute(0, 3, 1, 2).cpu()
         return out
 
+    def activation_list(self):
+        """[bool NCHW CPU tensor (value > 0) of the output region of every LeakyReLU- or
+        ReLU-activated op, in forward op order] for the last forward (test support: an
+        oracle that applies its activations in the same order consumes them one by one;
+        padded channels included, the caller slices the real ones)."""
+        out = []
+        for op in self.g.ops:
+            r = getattr(op, "out", None)
+            if r is None or getattr(op, "act", 0) not in (L.ACT_LRELU, L.ACT_RELU) or r.buf.t is None:
+                continue
+            out.append((r.buf.t[..., r.c0:r.c0 + r.c] > 0).permute(0, 3, 1, 2).cpu())
+        return out
+
     def _nonfinite(self):
         """names of buffers (activations / gradients) holding non-finite values (debug)."""
         out = set()
@@ -1710,10 +1761,8 @@ class Plan:
             L.check(lib.dvie_run_ops(base + start * sz, end - start, s), what)
             return
         for i in range(start, end):  # op-by-op with events (profiling steps only)
-            if arr[i].kind in (L.OP_FORK, L.OP_JOIN):
-                continue  # one stream here: the region markers order nothing
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            lane, arr[i].lane = arr[i].lane, 0  # on the timed stream: no fork / join in the timing
+            lane, arr[i].lane = arr[i].lane, 0  # on the timed stream: no side-stream wait in the timing
             e0.record()
             L.check(lib.dvie_run_ops(base + i * sz, 1, s), what)
             e1.record()

@@ -29,6 +29,7 @@ def _desc(kind, a, b, weight=1.0):
     d.b_sn, d.b_sc, d.b_sh, d.b_sw = b.stride()
     d.bsz, d.ch, d.h, d.w = a.shape
     d.weight = weight
+    d.out_scale = 1.0
     d.dtype = L.F32
     return d
 
@@ -151,6 +152,7 @@ def _metric(kind, a, b, ch, dtype=None, strides=None, weight=1.0):
     d.b_sn, d.b_sc, d.b_sh, d.b_sw = sb
     d.bsz, d.ch, d.h, d.w = a.shape[0], ch, a.shape[-2], a.shape[-1]
     d.weight = weight
+    d.out_scale = 1.0
     d.dtype = L.F32 if dtype is None else dtype
     part = torch.empty(max(1, lib.dvie_loss_partial_count(ctypes.byref(d))), dtype=torch.float64, device=a.device)
     out = torch.empty(1, dtype=torch.float32, device=a.device)

@@ -135,13 +135,6 @@ def _out_hw(conv, H, W):
     return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
 
 
-def _branch_lanes():
-    """DVIE_BRANCH_LANES=1: lower independent branches as branch regions (executor lanes 2..,
-    include/dvie.h).  Off by default: bit-identical, but measured neutral to -0.4% on the
-    bench step (same box, eager, profiles/r03v2/), while the weight lane alone gains."""
-    return os.environ.get("DVIE_BRANCH_LANES", "0") == "1"
-
-
 def _arg(args, name, default):
     return getattr(args, name, default) if args is not None else default
 
@@ -292,22 +285,15 @@ class HRNet(FlatParams, nn.Module):
         segs = []
         stem_c = 8 * F + rup(3 * F, 8) + self._stem_extra
         feat = g.buffer("feat", H, W, stem_c)
-        # the frames' segmentation encoders are independent chains into disjoint channel
-        # slices of the stem buffer: a branch region, one lane per frame
-        region = F > 1 and _branch_lanes()
-        if region:
-            g.fork()
         for k in range(F):
-            with g.lane(0 if k == 0 or not region else k + 1):
-                s_in = g.buffer(f"seg{k}_in", H, W, 24)
-                g.input_nchw(E.R(s_in), "seg", ext_c0=20 * k, ext_c=20)
-                e1 = g.buffer(f"seg{k}_e1", H, W, 32)
-                g.conv(E.R(s_in), self.seg_encoder[0], E.R(e1), act=A.ACT_ELU, name="seg_encoder.0")
-                e2 = g.buffer(f"seg{k}_e2", H, W, 32)
-                g.conv(E.R(e1), self.seg_encoder[2], E.R(e2), act=A.ACT_ELU, name="seg_encoder.2")
-                g.conv(E.R(e2), self.seg_encoder[4], E.R(feat, 8 * k, 8), name="seg_encoder.4")
-        if region:
-            g.join()
+            s_in = g.buffer(f"seg{k}_in", H, W, 24)
+            g.input_nchw(E.R(s_in), "seg", ext_c0=20 * k, ext_c=20)
+            e1 = g.buffer(f"seg{k}_e1", H, W, 32)
+            g.conv(E.R(s_in), self.seg_encoder[0], E.R(e1), act=A.ACT_ELU, name="seg_encoder.0")
+            e2 = g.buffer(f"seg{k}_e2", H, W, 32)
+            g.conv(E.R(e1), self.seg_encoder[2], E.R(e2), act=A.ACT_ELU, name="seg_encoder.2")
+            g.conv(E.R(e2), self.seg_encoder[4], E.R(feat, 8 * k, 8), name="seg_encoder.4")
+            g.segenc_chain(g.ops[-3:])  # one fused forward launch (engine Plan._segenc_fwd)
         # xgrad: the frames input needs a gradient (ExtraTrainer rollout feeds a prediction back)
         g.input_nchw(E.R(feat, 8 * F, rup(3 * F, 8)), "x", ext_c=3 * F, requires_grad=xgrad)
         if self._stem_extra:  # decoded VAE feature (its gradient feeds the decoder backward)
@@ -333,11 +319,6 @@ class HRNet(FlatParams, nn.Module):
         stages = [self.stage2, self.stage3] + ([self.stage4] if self.highres_large else [])
         for si, (tr, st) in enumerate(zip(trans, stages)):
             x_list = []
-            # several new branches read the same input: a branch region (their backwards sum
-            # into that input's gradient on lane 0 after the region)
-            region = sum(t is not None for t in tr) > 1 and _branch_lanes()
-            if region:
-                g.fork()
             for i, t in enumerate(tr):
                 if t is None:
                     x_list.append(y_list[i])
@@ -345,16 +326,13 @@ class HRNet(FlatParams, nn.Module):
                 # reference: transition1[i](x) (nets/HRNet.py:548-553), later transitions
                 # always read the last branch output (l.555-564)
                 cur = y_list[-1]
-                with g.lane(0 if i == 0 or not region else i + 1):
-                    for j, seq in enumerate(t if isinstance(t[0], nn.Sequential) else [t]):
-                        conv = seq[0]
-                        hh, ww = _out_hw(conv, cur.H, cur.W)
-                        ob = g.buffer(f"trans{si}.{i}.{j}", hh, ww, conv.out_channels)
-                        g.conv(cur, conv, E.R(ob), act=A.ACT_LRELU, name=f"transition{si + 1}.{i}")
-                        cur = E.R(ob)
+                for j, seq in enumerate(t if isinstance(t[0], nn.Sequential) else [t]):
+                    conv = seq[0]
+                    hh, ww = _out_hw(conv, cur.H, cur.W)
+                    ob = g.buffer(f"trans{si}.{i}.{j}", hh, ww, conv.out_channels)
+                    g.conv(cur, conv, E.R(ob), act=A.ACT_LRELU, name=f"transition{si + 1}.{i}")
+                    cur = E.R(ob)
                 x_list.append(cur)
-            if region:
-                g.join()
             last_stage = si == len(stages) - 1
             for mi, mod in enumerate(st):
                 x_list = self._hr_module(g, mod, x_list, f"stage{si + 2}.{mi}", final=last_stage and
@@ -394,19 +372,10 @@ class HRNet(FlatParams, nn.Module):
         A = L
         nbr = mod.num_branches
         xs = list(xs)
-        # the branches' block chains are independent (each reads and writes only its own
-        # resolution's buffers): a branch region, branch i on executor lane 0 / i + 1
-        # (concurrent HIP streams, forward and backward; DVIE_BRANCH_LANES=0: one stream)
-        region = nbr > 1 and _branch_lanes()
-        if region:
-            g.fork()
         for i in range(nbr):
-            with g.lane(0 if i == 0 or not region else i + 1):
-                for k, blk in enumerate(mod.branches[i]):
-                    assert blk.downsample is None
-                    xs[i] = self._basic(g, blk, xs[i], f"{name}.branches.{i}.{k}")
-        if region:
-            g.join()
+            for k, blk in enumerate(mod.branches[i]):
+                assert blk.downsample is None
+                xs[i] = self._basic(g, blk, xs[i], f"{name}.branches.{i}.{k}")
         if nbr == 1:
             return xs
         H, W = xs[0].H, xs[0].W
@@ -415,16 +384,8 @@ class HRNet(FlatParams, nn.Module):
             last = sum(x.c for x in xs)
             cat = g.buffer("cat", H, W, last)
         ys = []
-        # the fused outputs are independent (each reads the branch outputs and writes its own
-        # buffers); in the backward the branch outputs' gradients, which sum contributions
-        # of every lane, are summed on lane 0 after the region (engine: shared region inputs)
-        if region:
-            g.fork()
         for i in range(len(mod.fuse_layers)):
-            with g.lane(0 if i == 0 or not region else i + 1):
-                ys.append(self._fuse_output(g, mod, xs, i, cat, final, name))
-        if region:
-            g.join()
+            ys.append(self._fuse_output(g, mod, xs, i, cat, final, name))
         if not final:
             return ys
         # final upsample of every branch into the concat buffer
@@ -512,18 +473,10 @@ class HRNet(FlatParams, nn.Module):
             g.conv(cat, self.rgb_layer[0], hr, act=A.ACT_LRELU, name="rgb_layer.0")
             hs = E.R(g.buffer("seg_hidden", H, W, last))
             g.conv(cat, self.seg_layer[0], hs, act=A.ACT_LRELU, name="seg_layer.0")
-        # the two 3x3 output convs read disjoint hidden maps (or halves) and write separate
-        # outputs: a branch region (their data gradients write disjoint halves too)
-        region = _branch_lanes()
-        if region:
-            g.fork()
         rgb = g.buffer("rgb", H, W, E.rup(self.rgb_out_dim, 8), dtype=torch.float32, external=True)
         g.conv(hr, self.rgb_layer[2], E.R(rgb), name="rgb_layer.2")
         seg = g.buffer("segout", H, W, E.rup(self.seg_out_dim, 8), dtype=torch.float32, external=True)
-        with g.lane(2 if region else 0):
-            g.conv(hs, self.seg_layer[2], E.R(seg), name="seg_layer.2")
-        if region:
-            g.join()
+        g.conv(hs, self.seg_layer[2], E.R(seg), name="seg_layer.2")
         g.output("rgb", E.R(rgb), self.rgb_out_dim)
         g.output("segout", E.R(seg), self.seg_out_dim)
 

@@ -227,6 +227,7 @@ class VAEHRNet(HRNet):
             mu, logvar = PlanFunction.apply(self._fc, 1, code.reshape(n, 1024, 1, 1), *self._fc.params)
             if eps is None:
                 eps = torch.randn_like(mu)  # std.new(std.size()).normal_()
+            self.last_eps = eps  # the step's noise (test support: the oracle replays it)
             z = _ReparamFn.apply(mu, logvar, eps.to(mu.device))
         else:  # torch.zeros(bs, 1024).normal_()
             z = (torch.randn(n, 1024, device=x.device) if eps is None else eps.to(x.device)).float()

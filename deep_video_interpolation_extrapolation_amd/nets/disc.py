@@ -180,6 +180,7 @@ class _PlanDiscriminator(FlatParams, nn.Module):
 
     in_keys = ()
     local = False  # True: the last conv's (B, 1, h, w) map is the output (no AvgPool head)
+    plan_log = None  # test support: a list collects the plan of every forward call, in order
 
     def _finish_init(self):
         self.dtype = precision_of(self.args)
@@ -284,6 +285,8 @@ class _PlanDiscriminator(FlatParams, nn.Module):
             plan.set_head_output("score", out)
         plan.run_forward()
         self.last_plan = plan
+        if self.plan_log is not None:
+            self.plan_log.append(plan)
         if self.training:  # one increment per BatchNorm call, as nn.BatchNorm2d.train()
             for op in plan.g.ops:
                 if isinstance(op, E.BNOp) and op.m.num_batches_tracked is not None:

@@ -218,6 +218,7 @@ class SRNRefine(FlatParams, nn.Module):
             plan.set_output_nchw(f"pred{i}", t)
             outs.append(t)
         plan.run_forward()
+        self.last_plan = plan
         return plan, tuple(outs)
 
     def run_backward(self, plan, inputs, grads, needs):

@@ -73,6 +73,8 @@ def vgg19_features(weights=None):
 class my_vgg(nn.Module):
     """Reference nets/vgg.py:5-54: five ReLU feature maps, AvgPool2d(2,2) between blocks."""
 
+    sign_log = None  # test support: a list collects the ReLU branches of every loss call, in order
+
     def __init__(self, vgg):
         super().__init__()
         self.vgg = vgg
@@ -131,6 +133,8 @@ class my_vgg(nn.Module):
         plan.set_input("gt", gt)
         plan.run_forward()
         self.last_plan = plan
+        if self.sign_log is not None:
+            self.sign_log.append(plan.activation_signs())
         return plan, (plan.l1_out[:len(FEATURE_TAPS)].sum() / len(FEATURE_TAPS),)
 
     def run_backward(self, plan, inputs, grads, needs):
@@ -155,6 +159,8 @@ class my_vgg(nn.Module):
             plan.set_input("gt", gt)
             plan.set_l1_loss(out, value_scale, grad_scale)
             plan.run_forward()
+            if self.sign_log is not None:  # before a later loss call reuses the plan
+                self.sign_log.append(plan.activation_signs())
             plan.set_input_grad("pred", grad, accumulate=accumulate)
             plan.run_backward()
         finally:

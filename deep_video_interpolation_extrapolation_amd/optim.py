@@ -53,6 +53,11 @@ class _FusedOptimizer(torch.optim.Optimizer):
         """one device step tensor shared by `params` (created from their host count)"""
         d = self._dsteps.get(key)
         if d is None or d.device != device:
+            if torch.cuda.is_current_stream_capturing():
+                # a count created here would be re-initialised by every replay
+                raise RuntimeError("capturable optimizer: a parameter takes its first step inside the captured "
+                                   "step (e.g. SpectralNorm u / v, trainable from the second step): run more "
+                                   "eager warm-up steps before capturing")
             st = self.state[params[0]]
             d = torch.full((1,), float(st.get("step", 0.0)), dtype=torch.float32, device=device)
             self._dsteps[key] = d
@@ -60,18 +65,25 @@ class _FusedOptimizer(torch.optim.Optimizer):
             self.state[p]["step"] = d
         return d
 
-    def _counts_differ(self, gi, ps):
-        """Whether the group's parameters carry different step counts.  Eager: checked on
-        the host counts every step.  Capturable: decided once, on the host counts of the
-        first (eager) step after set_capturable, and kept -- counts that differ once keep
-        differing by the same lag, and a captured step must not read device counts back."""
-        if self.capturable and gi in self._split:
-            return self._split[gi]
+    def _host_counts_differ(self, ps):
         counts = set()
         for p in ps:
             st = self.state[p].get("step", 0.0)
             counts.add(float(st.cpu()) if torch.is_tensor(st) else float(st))
-        differ = len(counts) > 1
+        return len(counts) > 1
+
+    def _counts_differ(self, gi, ps):
+        """Whether the group's parameters carry different step counts.  Eager: checked on
+        the host counts every step.  Capturable: decided on the host counts by the first
+        eager step after set_capturable (whether or not every parameter had a gradient then,
+        see step()) and kept -- counts that differ once keep differing by the same lag, and a
+        captured step must not read device counts back."""
+        if self.capturable and gi in self._split:
+            return self._split[gi]
+        if self.capturable and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("capturable optimizer: run one eager step after set_capturable(True) "
+                               "before capturing a step")
+        differ = self._host_counts_differ(ps)
         if self.capturable:
             self._split[gi] = differ
         return differ
@@ -156,6 +168,13 @@ class _FusedOptimizer(torch.optim.Optimizer):
                     continue
                 st["step"] += 1
                 self._launch(p, g, st[k0], st[k1], p.numel(), group, float(st["step"]), p.device)
+        if self.capturable and not torch.cuda.is_current_stream_capturing():
+            # decide every group's split after this eager step, also for a group whose
+            # parameters were not all stepped (e.g. SpectralNorm u / v without gradients yet),
+            # so that the captured step never reads the step counts back
+            for gi, group in enumerate(self.param_groups):
+                if gi not in self._split:
+                    self._split[gi] = self._host_counts_differ(group["params"])
         return loss
 
     def load_state_dict(self, state_dict):

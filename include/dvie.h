@@ -277,8 +277,8 @@ int dvie_ew(const dvie_ew_desc* d, void* stream);
 /*
  * grad (L1, GDL, SSIM, CE): d(weight * loss)/d(a), NCHW-contiguous fp32; beta = 1 adds it
  * to what grad holds (several losses of one prediction write one gradient buffer).
- * out: the loss value times out_scale (0 is read as 1, so zero-initialised descriptors
- * report the plain value); out_acc = 1 adds it to *out instead of storing it (the five
+ * out: the loss value times out_scale, taken as given (a weight-0 term reports 0; builders
+ * set 1.0 for the plain value); out_acc = 1 adds it to *out instead of storing it (the five
  * VGG feature levels into one scalar).  weight scales the gradient only (COSNHWC: the value).
  */
 typedef struct dvie_loss_desc {
@@ -546,22 +546,74 @@ typedef struct dvie_attn_desc {
 int dvie_attn(const dvie_attn_desc* d, void* stream);
 
 /*
+ * Fused backward of a narrow-output 3x3 stride-1 conv over a LeakyReLU-activated map: the
+ * HRNet output heads rgb_layer[2] / seg_layer[2] (448 -> 3 / 448 -> 20, reference
+ * nets/HRNet.py:410-442, 584-588), whose backward is nn.Conv2d backward-data + the preceding
+ * LeakyReLU's derivative + nn.Conv2d backward-weight.  One pass over the hidden map h:
+ *   dh[p][ci]  = act'(h[p][ci]) * sum_{t, o} wd[ci][t * cout + o] * g[p + (dy0 + i_t, dx0 + j_t)][o]
+ *   ws[s][o][(8 - t) * c + ci] = sum_{p in split s} g[p + (dy0 + i_t, dx0 + j_t)][o] * h[p][ci]
+ * (t = 3 i_t + j_t the data-gradient tap; 8 - t the forward tap of the same weight), so
+ * h is read once and the dh map written once; the weight-gradient partial slabs have the
+ * dvie_conv2d_wgrad layout (reduce them with dvie_wgrad_reduce, ws_k = 9 * c).
+ * g: (n, h, w, cout) bf16 NHWC output gradient (cout 8 or 24, padded channels zero);
+ * h: the conv input (bf16 NHWC, c channels, a multiple of 64); wd: the packed data-gradient
+ * weights [c][kpad] (dvie_pack_weights mode 1: wd[ci][t * cout + o] = w[o][ci][2 - i_t][2 - j_t]);
+ * dh: bf16 NHWC, written (not accumulated); dact: DVIE_ACT_LRELU (alpha) or DVIE_ACT_NONE.
+ * splits: weight-gradient slabs (grid = (c / 64) * splits workgroups); bf16 only.
+ */
+typedef struct dvie_head3_bwd_desc {
+  const void* g;
+  const void* h;
+  const void* wd;
+  void* dh;
+  float* ws;
+  long long g_ld, h_ld, dh_ld;
+  int n, hgt, wid, c;
+  int cout, kpad, dy0, dx0;
+  int splits, dact;
+  float alpha, pad0;
+} dvie_head3_bwd_desc;
+
+int dvie_head3_bwd(const dvie_head3_bwd_desc* d, void* stream);
+
+/*
+ * Fused forward of HRNet's segmentation encoder (reference nets/HRNet.py:358-364, applied at
+ * l.533-537): e1 = ELU(conv3x3(in) + b0) (24 -> 32 channels; the 20 classes padded to 24),
+ * e2 = ELU(conv3x3(e1) + b2) (32 -> 32), out = conv3x3(e2) + b4 (32 -> 8: the 4 encoder
+ * channels + 4 zero-weight pads), stride 1, zero padding, bf16 NHWC.  e1 and e2 are written
+ * (the backward reads them); out may be a channel slice of a wider buffer (out_ld).  w0 / w2 /
+ * w4: the forward-packed weights [cout][kpad] (dvie_pack_weights mode 0: w[co][t * cin + ci]),
+ * b0 / b2 / b4: fp32 biases (32, 32, 8).
+ */
+typedef struct dvie_segenc_desc {
+  const void* in;
+  void* e1;
+  void* e2;
+  void* out;
+  const void* w0;
+  const void* w2;
+  const void* w4;
+  const float* b0;
+  const float* b2;
+  const float* b4;
+  long long in_ld, e1_ld, e2_ld, out_ld;
+  int n, h, w, kpad0;
+  int kpad2, kpad4;
+} dvie_segenc_desc;
+
+int dvie_segenc_fwd(const dvie_segenc_desc* d, void* stream);
+
+/*
  * Op-list executor: runs n descriptors in order with a single host call (the per-step
  * forward and backward plans of the HRNet / VGG executors).  dvie_op.lane picks the stream:
  *   0     the caller's stream;
  *   1     the weight lane (a library side stream of the current device and host thread):
  *         work off the critical path (weight gradients and their reductions).  A run of
- *         lane-1 ops first waits for everything issued so far on the stream of the last
- *         lane-0 / branch-lane op (the data lane that produced its inputs);
- *   2..7  branch lanes (library side streams): independent branches of a network (HRNet's
- *         resolution branches).  DVIE_OP_FORK (no payload) marks the start of a branch
- *         region: each branch lane's first op after it waits for everything issued on the
- *         caller's stream before the FORK; DVIE_OP_JOIN makes the caller's stream wait for
- *         the branch lanes used since the FORK.  Lane-0 ops inside a region run on the
- *         caller's stream as one of the branches.
- * The call ends with the caller's stream waiting for every side stream it used, so the call
- * as a whole is ordered on the caller's stream; it is capturable (forks and joins become
- * graph edges).  DVIE_OP_LANES=0 runs every op on the caller's stream.
+ *         lane-1 ops first waits for everything issued so far on the caller's stream (the
+ *         lane-0 ops that produced its inputs), so lane-1 ops read only finished data.
+ * The call ends with the caller's stream waiting for the side stream if it was used, so the
+ * call as a whole is ordered on the caller's stream and capturable (the wait is a graph
+ * edge).  DVIE_OP_LANES=0 runs every op on the caller's stream.
  */
 #define DVIE_OP_CONV 1
 #define DVIE_OP_WGRAD 2
@@ -575,8 +627,8 @@ int dvie_attn(const dvie_attn_desc* d, void* stream);
 #define DVIE_OP_HEAD_FWD 10
 #define DVIE_OP_HEAD_BWD 11
 #define DVIE_OP_ATTN 12
-#define DVIE_OP_FORK 13 /* branch-region markers (no payload), see above */
-#define DVIE_OP_JOIN 14
+#define DVIE_OP_HEAD3_BWD 13
+#define DVIE_OP_SEGENC_FWD 14
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
@@ -585,7 +637,7 @@ typedef struct dvie_pack_list {
 
 typedef struct dvie_op {
   int kind;
-  int lane; /* 0: caller's stream, 1: weight lane, 2..7: branch lanes (see above) */
+  int lane; /* 0: caller's stream, 1: weight lane (see above) */
   union {
     dvie_conv_desc conv;
     dvie_wgrad_desc wgrad;
@@ -597,6 +649,8 @@ typedef struct dvie_op {
     dvie_bn_desc bn;
     dvie_head_desc head;
     dvie_attn_desc attn;
+    dvie_head3_bwd_desc head3;
+    dvie_segenc_desc segenc;
   } u;
 } dvie_op;
 

@@ -120,8 +120,23 @@ def _up(x, size=None, scale=None):
 
 
 class _Net:
-    def __init__(self, P, specs):
+    """masks: the implementation's LeakyReLU branches, one bool NCHW tensor per activation in
+    the order this restatement applies them (Plan.activation_list), imposed on the oracle so
+    an fp64 evaluation follows the same branches (see hrnet._lrelu)."""
+
+    def __init__(self, P, specs, masks=None):
         self.P, self.g = P, _geo(specs)
+        self.masks = None if masks is None else iter(masks)
+
+    def act(self, x):
+        if self.masks is None:
+            return _lrelu(x)
+        m = next(self.masks)[:, :x.shape[1]].to(x.device)
+        assert m.shape == x.shape, (m.shape, x.shape)
+        return torch.where(m, x, 0.2 * x)
+
+    def done(self):
+        assert self.masks is None or next(self.masks, None) is None, "unused activation masks"
 
     def conv(self, name, x):
         kind, s, p, d = self.g[name]
@@ -131,21 +146,21 @@ class _Net:
         return F.conv2d(x, w, b, stride=s, padding=p, dilation=d)
 
     def res(self, name, x):  # ResnetBlock: conv-LReLU-conv + input (refine_nets.py:14-24)
-        return self.conv(name + ".conv.2", _lrelu(self.conv(name + ".conv.0", x))) + x
+        return self.conv(name + ".conv.2", self.act(self.conv(name + ".conv.0", x))) + x
 
     def seq(self, names_acts, x):
         for n, act in names_acts:
             x = self.conv(n, x) if not n.endswith("!res") else self.res(n[:-4], x)
             if act:
-                x = _lrelu(x)
+                x = self.act(x)
         return x
 
 
-def srn_forward(P, input_rgb, input_seg, encoded_feat, n_scales):
+def srn_forward(P, input_rgb, input_seg, encoded_feat, n_scales, masks=None):
     """SRNRefine.forward: per scale (coarsest first) input [rgb, previous prediction
     (2x up, detached), seg + encoded features] at that scale -> prediction; the hidden
     bottleneck state is carried (2x up, not detached) to the next scale."""
-    N = _Net(P, srn_specs())
+    N = _Net(P, srn_specs(), masks)
     others = torch.cat([input_seg, encoded_feat], 1)
     preds, hidden = [], []
     for si in range(n_scales - 1, -1, -1):
@@ -167,6 +182,7 @@ def srn_forward(P, input_rgb, input_seg, encoded_feat, n_scales):
         out = N.seq([(f"output_layer.{i}!res", 0) for i in (0, 1, 2)] + [("output_layer.3", 1), ("output_layer.5", 0)],
                     d1 + il)
         preds.append(out)
+    N.done()
     return preds
 
 
@@ -226,9 +242,9 @@ def weighted_neighbours_low(f1, f2, prob):
     return outs
 
 
-def attn_forward(P, coarse_img, coarse_seg, neighbors_img, neighbors_seg, n_scales, prop):
+def attn_forward(P, coarse_img, coarse_seg, neighbors_img, neighbors_seg, n_scales, prop, masks=None):
     """MSResAttnRefine.forward (refine_nets.py:325-399) -> (outputs per scale, flow maps)."""
-    N = _Net(P, attn_specs())
+    N = _Net(P, attn_specs(), masks)
     x_comb = torch.cat([coarse_img, coarse_seg], 1)
     f_comb = torch.cat([neighbors_img[:, :3], neighbors_seg[:, :20]], 1)
     b_comb = torch.cat([neighbors_img[:, 3:6], neighbors_seg[:, 20:40]], 1)
@@ -266,16 +282,18 @@ def attn_forward(P, coarse_img, coarse_seg, neighbors_img, neighbors_seg, n_scal
         d2 = N.seq([("decoder_2.0", 1), ("decoder_2.2!res", 0)], fu)
         d1 = N.seq([("decoder_1.0", 1), ("decoder_1.2!res", 0)], d2 + ie1)
         outs.append(N.seq([("output_layer.0", 1), ("output_layer.2", 1), ("output_layer.4", 0)], d1 + ii))
+    N.done()
     return outs, flows
 
 
-def inter_refine_forward(Pc, Pr, x, seg, n_scales, Ps=None, prop=False):
+def inter_refine_forward(Pc, Pr, x, seg, n_scales, Ps=None, prop=False, masks=None, rmasks=None, smasks=None):
     """InterRefineNet (Ps None) / InterStage3Net forward (nets/InterRefineNet.py:15-53),
     train split: coarse HRNet, softmax of its seg logits (detached), the coarse seg
     encoder re-run on both input segs (detached), SRNRefine on the clamped detached coarse
     image; refine outputs clamped to [-10, 10] (InterRefineNet) or [-1, 1] (InterStage3Net,
-    which then runs the stage-3 net on the last refine output, clamped to [-10, 10])."""
-    rgb, seg_out = H.forward(Pc, torch.cat([x, seg], 1))
+    which then runs the stage-3 net on the last refine output, clamped to [-10, 10]).
+    masks / rmasks / smasks: imposed activation branches of the coarse / refine / stage-3 nets."""
+    rgb, seg_out = H.forward(Pc, torch.cat([x, seg], 1), masks=masks)
     soft = torch.softmax(seg_out, 1).detach()
 
     def segenc(s):
@@ -284,9 +302,9 @@ def inter_refine_forward(Pc, Pr, x, seg, n_scales, Ps=None, prop=False):
         return F.conv2d(h, Pc["seg_encoder.4.weight"], Pc["seg_encoder.4.bias"], padding=1)
 
     enc = torch.cat([x, segenc(seg[:, :20]).detach(), segenc(seg[:, 20:40]).detach()], 1)
-    refine = srn_forward(Pr, rgb.detach().clamp(-1, 1), soft, enc, n_scales)
+    refine = srn_forward(Pr, rgb.detach().clamp(-1, 1), soft, enc, n_scales, masks=rmasks)
     if Ps is None:
         return rgb, seg_out, [r.clamp(-10, 10) for r in refine]
     refine = [r.clamp(-1, 1) for r in refine]
-    outs, flows = attn_forward(Ps, refine[-1].detach(), soft, x, seg, n_scales, prop)
+    outs, flows = attn_forward(Ps, refine[-1].detach(), soft, x, seg, n_scales, prop, masks=smasks)
     return rgb, seg_out, refine, [o.clamp(-10, 10) for o in outs], flows

@@ -30,6 +30,12 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
                      maps, parameter-gradient stats for seeded output gradients
   clip_crops.npz G13: reference get_seq_crop_params (folder.py:125-149) crops and the
                      flip draw (folder.py:211) for seeds 0..63
+  gan_vae.npz    G14: two InterGANTrainer steps (runners/InterGANTrainer.py:376-456 body) of
+                     the reference's own runnable InterGAN configuration: InterGANNet with a
+                     VAEHRNet coarse model (KLD term) and FrameSN / VideoSN discriminators
+                     (seg_disc), 128x128, batch 2; step 2 with SpectralNorm u / v trainable
+                     (set_net_grad(True)): loss dicts, gradient stats, post-step checksums, u / v,
+                     BatchNorm running statistics
 """
 import os
 import sys
@@ -401,9 +407,74 @@ def g12():
     np.savez_compressed(os.path.join(HERE, "clip_crops.npz"), crops=np.array(crops), flips=np.array(flips))
 
 
+def g14():
+    """The reference's InterGAN step body composed from its own modules (InterGANNet forward,
+    RGBLoss on (x + 1) / 2, 30 * CrossEntropy, KLDLoss, GANScalarLoss, Adamax / Adam), W = 1.
+    The reparameterisation noise of step k is the CPU draw right after torch.manual_seed(78 + k)
+    (inputs.vae_eps(2, 78 + k)): the coarse model's reparameterize is the forward's first RNG use.
+    `Tensor.cuda` is the identity here (InterGANNet.py:35 moves a zero tensor to the GPU)."""
+    args = args_ns(coarse_model="VAEHRNet", frame_disc=True, video_disc=True, frame_det_disc=False,
+                   video_det_disc=False, track_gen=False, frame_disc_model="FrameSNDiscriminator",
+                   video_disc_model="VideoSNDiscriminator", seg_disc=True, rank=0, kld_weight=20.0, vae=True)
+    cuda0 = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        torch.manual_seed(1024)
+        model = ref_nets.InterGANNet(args)
+        model.train()
+        rgb_loss = ref_losses.RGBLoss(args)
+        kld = ref_losses.KLDLoss(args)
+        ce = torch.nn.CrossEntropyLoss()
+        d_loss, g_loss = ref_losses.GANScalarLoss(weight=1.0), ref_losses.GANScalarLoss(weight=1.0)
+        coarse_opt = torch.optim.Adamax(list(model.coarse_model.parameters()), lr=1e-3)
+        frame_opt = torch.optim.Adam(list(model.frame_disc_model.parameters()), lr=1e-3)
+        video_opt = torch.optim.Adam(list(model.video_disc_model.parameters()), lr=1e-3)
+        out = {}
+        for mod, tag in ((model.coarse_model, "g"), (model.frame_disc_model, "f"), (model.video_disc_model, "v")):
+            out[tag + "_init_names"], out[tag + "_init"] = checksums(dict(mod.state_dict()))
+        data = inputs.step_batch(2, 128, 128)
+        for k in range(2):
+            gt_x, gt_seg = data["frame2"], data["seg2"]
+            x = torch.cat([data["frame1"], data["frame3"]], dim=1)
+            seg = torch.cat([data["seg1"], data["seg3"]], dim=1)
+            torch.manual_seed(78 + k)
+            res = model(x, seg, gt_x, gt_seg, bboxes=data.get("bboxes"))
+            coarse_img, coarse_seg, mu, logvar = res[:4]
+            dff, drf, dfv, drv, gff, gfv = res[4:10]
+            norm = lambda t: (t + 1) / 2  # noqa: E731  InterGANTrainer.normalize
+            ld = rgb_loss(norm(coarse_img), norm(gt_x), False, prefix="coarse")
+            ld["coarse_ce_loss"] = args.ce_weight * ce(coarse_seg, torch.argmax(gt_seg, dim=1))
+            ld["coarse_kld_loss"] = kld(mu, logvar)
+            ld["coarse_frame_loss"] = g_loss(gff, True)
+            ld["disc_frame_real_loss"] = d_loss(drf, True)
+            ld["disc_frame_fake_loss"] = d_loss(dff, False)
+            ld["coarse_video_loss"] = g_loss(gfv, True)
+            ld["disc_video_real_loss"] = d_loss(drv, True)
+            ld["disc_video_fake_loss"] = d_loss(dfv, False)
+            loss = 0
+            for v in ld.values():
+                loss += torch.mean(v)
+            ld["loss_all"] = loss
+            for o in (coarse_opt, frame_opt, video_opt):
+                o.zero_grad()
+            loss.backward()
+            t = f"step{k + 1}_"
+            out[t + "loss_names"] = np.array(list(ld.keys()))
+            out[t + "loss_values"] = np.array([float(v) for v in ld.values()])
+            for mod, tag in ((model.coarse_model, "g"), (model.frame_disc_model, "f"), (model.video_disc_model, "v")):
+                out[t + tag + "_grad_names"], out[t + tag + "_grad_stats"] = _gstats(mod)
+            for o in (coarse_opt, frame_opt, video_opt):
+                o.step()
+            for mod, tag in ((model.coarse_model, "g"), (model.frame_disc_model, "f"), (model.video_disc_model, "v")):
+                out[t + tag + "_post_names"], out[t + tag + "_post"] = checksums(dict(mod.state_dict()))
+        np.savez_compressed(os.path.join(HERE, "gan_vae.npz"), **out)
+    finally:
+        torch.Tensor.cuda = cuda0
+
+
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11, g12)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11, g12, g14)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()

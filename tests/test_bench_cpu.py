@@ -39,3 +39,16 @@ def test_gpus_n_spawns_child_torchrun(monkeypatch):
     (cmd, env), = calls
     assert "--nproc-per-node=2" in cmd and cmd[-4:] == ["--gpus", "2", "--steps", "3"]
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_refuses_timing_switches():
+    """A DVIE_*_DBG variable (timing-only kernel ablations, wrong results) makes bench.py exit
+    non-zero before anything runs."""
+    import bench
+    with pytest.raises(SystemExit) as e:
+        bench.refuse_timing_switches({"DVIE_HALO_DBG": "8"})
+    assert e.value.code == 2
+    bench.refuse_timing_switches({"DVIE_HALO_DBG": "", "DVIE_1X1_DBG": "0", "DVIE_PRECISION": "bf16"})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], capture_output=True,
+                       text=True, env=dict(os.environ, DVIE_1X1_DBG="2"), timeout=120)
+    assert r.returncode == 2 and "DVIE_1X1_DBG" in r.stderr

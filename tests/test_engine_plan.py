@@ -58,11 +58,17 @@ def test_hrnet_plan_structure(dtype, fused, monkeypatch):
     assert len(heads) == int(fused)
     if fused:
         assert sorted(heads[0].expected) == [(0, 448), (448, 448)] and heads[0].dact_done
-    # every trainable conv gets one wgrad; stride-2 dgrads split into 4 phases
-    assert kinds[L.OP_WGRAD] == n_ref
+    # every trainable conv gets one wgrad; stride-2 dgrads split into 4 phases; in bf16 the
+    # two 3x3 output heads' data + weight gradients are one fused launch each (dvie_head3_bwd)
+    # ... and the two frames' segmentation encoders run their three forward convs as one
+    # launch each (dvie_segenc_fwd)
+    n_head3 = n_seg = 2 if dtype == torch.bfloat16 else 0
+    assert kinds.get(L.OP_HEAD3_BWD, 0) == n_head3
+    assert kinds.get(L.OP_SEGENC_FWD, 0) == n_seg
+    assert kinds[L.OP_WGRAD] == n_ref - n_head3
     n_s2 = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2)
     n_dgrad = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.x.buf.needs_grad)
-    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2
+    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2 - n_head3 - 3 * n_seg
     # every buffer that needs a gradient received all of its contributions
     for b in g.buffers:
         if b.needs_grad and b.expected:
@@ -143,100 +149,24 @@ def test_buckets_with_unstacked_heads(bucket_mb, monkeypatch):
         assert len(cuts) >= 2
 
 
-@pytest.mark.parametrize("dtype,im2col", [(torch.float32, "0"), (torch.bfloat16, "0"), (torch.bfloat16, "1")])
-def test_branch_regions_are_independent(dtype, im2col, monkeypatch):
-    """HRNet's branch regions (ForkOp ... JoinOp, one executor lane per resolution branch
-    and per output head, include/dvie.h dvie_op.lane): in the forward graph and in the
-    compiled backward descriptors, no channel range one branch lane writes is read or
-    written by another branch lane inside the region (the weight lane, 1, only reads);
-    markers pair up in both lists; the weight-gradient ops are on the weight lane."""
-    monkeypatch.setenv("DVIE_BRANCH_LANES", "1")
-    monkeypatch.setenv("DVIE_WGRAD_LANE", "1")
-    monkeypatch.setenv("DVIE_IM2COL_DGRAD", im2col)  # (its scratch buffers must be per lane)
-    hr = make().coarse_model
-    g = hr._lower(E.Graph(dtype), 32, 64)
-    plan = g.compile(2, torch.device("cpu"), backward=True)
-
-    def overlap(u, v):  # (tensor, c0, c1) accesses
-        return u[0] == v[0] and u[1] < v[2] and v[1] < u[2]
-
-    def check(groups):
-        for a in groups:
-            for b in groups:
-                if a != b:
-                    wa, (rb, wb) = groups[a][1], groups[b]
-                    bad = [(u, v) for u in wa for v in rb + wb if overlap(u, v)]
-                    assert not bad, (a, b, bad[:3])
-
-    # forward graph
-    n_regions, n_bwd_regions, groups = 0, 0, None
-    for op in g.ops:
-        if isinstance(op, E.JoinOp):
-            check(groups)
-            groups = None
-        elif isinstance(op, E.ForkOp):
-            n_regions += 1
-            n_bwd_regions += int(op.backward)
-            groups = {}
-        elif groups is not None:
-            r, w = groups.setdefault(op.lane, ([], []))
-            r.extend((id(x.buf), x.c0, x.c0 + x.c) for x in op.inputs())
-            if op.out is not None:
-                w.append((id(op.out.buf), op.out.c0, op.out.c0 + op.out.c))
-    # the two frames' segmentation encoders, the branch blocks of stage 2 (2 branches) and
-    # stage 3 (3), the two output heads, transition1's two new branches, the fused outputs of
-    # stages 2 and 3
-    assert (n_regions, n_bwd_regions) == (7, 7) and groups is None
-
-    # backward descriptors: pointers mapped to channel ranges of the plan's buffers
-    spans = []
-    for b in g.buffers:
-        for t in (b.t, b.g):
-            if t is not None:
-                spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), id(t), t.element_size(), b.C))
-    for t in plan.keep:  # scratch and packed weights: one range each
-        if isinstance(t, torch.Tensor) and t.numel():
-            spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), id(t), t.element_size(),
-                          1 << 40))
-
-    def acc(p, c):
-        if not p:
-            return None
-        for lo, hi, k, es, C in spans:
-            if lo <= p < hi:
-                c0 = (p - lo) // es % C
-                return (k, c0, c0 + c)
-        return None
-
-    kinds = [plan.bwd_arr[i].kind for i in range(plan.n_bwd)]
-    assert kinds.count(L.OP_FORK) == kinds.count(L.OP_JOIN) == 7
-    groups = None
-    for i in range(plan.n_bwd):
-        o = plan.bwd_arr[i]
-        if o.kind == L.OP_FORK:
-            assert groups is None
-            groups = {}
-            continue
-        if o.kind == L.OP_JOIN:
-            check(groups)
-            groups = None
-            continue
-        if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM):
-            assert o.lane == 1
-            continue
-        if groups is None:
-            assert o.lane == 0
-            continue
-        assert o.kind in (L.OP_CONV, L.OP_EW), o.kind
-        r, w = groups.setdefault(o.lane, ([], []))
-        if o.kind == L.OP_CONV:
-            d = o.u.conv
-            reads = [(d.x, d.c), (d.res, d.cout), (d.z, d.cout)] + ([(d.y, d.cout)] if d.beta else [])
-            w.append(acc(d.y, d.cout))
-        else:
-            d = o.u.ew
-            reads = [(d.src0, d.c), (d.src1, d.c), (d.src2, d.c), (d.res, d.c), (d.z, d.c)] + \
-                ([(d.y, d.c)] if d.beta else [])
-            w.append(acc(d.y, d.c))
-        r.extend(a for a in (acc(p, c) for p, c in reads) if a is not None)
-    assert groups is None
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_weight_lane_tags(dtype, monkeypatch):
+    """Executor lanes of a compiled HRNet plan (include/dvie.h dvie_op.lane): every weight /
+    bias gradient op (WGRAD, WREDUCE, COLSUM) is on the weight lane 1 and every other op, in
+    both directions, on the caller's stream (lane 0); DVIE_WGRAD_LANE=0 puts everything on
+    lane 0."""
+    for env, wl in (("1", 1), ("0", 0)):
+        monkeypatch.setenv("DVIE_WGRAD_LANE", env)
+        hr = make().coarse_model
+        g = hr._lower(E.Graph(dtype), 32, 64)
+        plan = g.compile(2, torch.device("cpu"), backward=True)
+        n_w = 0
+        for i in range(plan.n_bwd):
+            o = plan.bwd_arr[i]
+            if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM):
+                assert o.lane == wl
+                n_w += 1
+            else:
+                assert o.lane == 0, o.kind
+        assert n_w > 50
+        assert all(plan.fwd_arr[i].lane == 0 for i in range(len(plan.fwd_arr)))

@@ -49,23 +49,36 @@ def _trainer(**kw):
 
 
 @pytest.mark.timeout(300)
-def test_extra_stage3_step_matches_oracle(dev):
+def test_extra_stage3_step_matches_oracle(dev, monkeypatch):
+    """Loss dict 1e-4; every gradient tensor of the three nets within 1e-4 relative L2 of the
+    fp64 oracle evaluated on this step's branches (coarse HRNet LeakyReLUs, refine and stage-3
+    activation lists, the ReLUs of each VGG-loss call); post-Adamax weights."""
+    from deep_video_interpolation_extrapolation_amd.nets.vgg import my_vgg
     tr = _trainer(n_scales=2, stage3_prop=True, batch_size=2, input_h=64, input_w=128, synthetic=2,
                   precision="fp32")
     data = OS.synthetic_batch(2, 64, 128)
+    monkeypatch.setattr(my_vgg, "sign_log", [])
     ld = tr.step(data)
+    vmasks = my_vgg.sign_log
     Pc = OH.init_params(1024)
     Pr = OR.init_params(None, OR.srn_specs())
     Ps = OR.init_params(None, OR.attn_specs())
-    ref, grads, new = OS.extra_refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps, prop=True)
+    ref, _, new = OS.extra_refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps, prop=True)
     assert list(ld.keys()) == list(ref.keys()), (list(ld.keys()), list(ref.keys()))
     np.testing.assert_allclose([float(ld[k]) for k in ref], [ref[k] for k in ref], rtol=1e-4)
     m = tr.model.module
+    _, g64, _ = OS.extra_refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps, prop=True,
+                                     masks=m.coarse_model.last_plan.activation_signs(),
+                                     rmasks=m.refine_model.last_plan.activation_list(),
+                                     smasks=m.stage3_model.last_plan.activation_list(), vmasks=vmasks,
+                                     dtype=torch.float64)
     for part, mod in (("coarse", m.coarse_model), ("refine", m.refine_model), ("stage3", m.stage3_model)):
         named = dict(mod.named_parameters())
-        errs = [rel_l2(named[k].grad, g) for k, g in grads[part].items()]
-        print(f"{part}: gradient relative L2 median {np.median(errs):.2e} worst {max(errs):.2e}")
-        assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (part, float(np.median(errs)), max(errs))
+        errs = {k: rel_l2(named[k].grad, g) for k, g in g64[part].items()}
+        worst = max(errs, key=errs.get)
+        print(f"C5-net step {part}: gradients vs fp64 oracle on the same branches: relative L2 median "
+              f"{np.median(list(errs.values())):.2e}, worst {errs[worst]:.2e} ({worst})")
+        assert errs[worst] <= 1e-4, (part, worst, errs[worst])
         moved = sum(int(((named[k].detach().cpu() - w).abs() > 1e-4).sum()) for k, w in new[part].items())
         total = sum(w.numel() for w in new[part].values())
         assert moved <= 1e-3 * total, (part, moved, total)

@@ -190,10 +190,14 @@ def test_adam_matches_torch101_form(dev):
 
 
 def test_intergan_step_matches_oracle(dev):
-    """InterGANTrainer (HRNet + FrameDiscriminator + VideoDiscriminator, seg_disc) one fp32
-    step at 128x128 vs oracle.step.gan_step: loss dict 1e-4 relative; post-update weight
-    sums of squares 1e-4 relative (generator) / 1e-3 (discriminators, excluding the
-    zero-gradient BatchNorm-preceding conv biases, which Adam moves by +-lr on noise)."""
+    """InterGANTrainer (HRNet coarse model + FrameDiscriminator + VideoDiscriminator, seg_disc:
+    the build-defined form that runs at any size) one fp32 step at 128x128 vs
+    oracle.step.gan_step: loss dict 1e-4 relative; every generator and discriminator gradient
+    against the fp64 oracle on this step's activation branches (all six discriminator passes
+    imposed) within 1e-4 relative L2, 3e-4 where the gradient comes back through the
+    discriminators' train-mode BatchNorm (all discriminator tensors, the generator's through the
+    G passes); post-update weights within 1e-4 except a 1e-3 fraction (first Adamax / Adam step:
+    +-lr on the sign of a near-zero gradient)."""
     os.environ["DVIE_PRECISION"] = "fp32"
     from deep_video_interpolation_extrapolation_amd.options import default_args
     from deep_video_interpolation_extrapolation_amd.runners.InterGANTrainer import InterGANTrainer
@@ -216,61 +220,191 @@ def test_intergan_step_matches_oracle(dev):
                 for k in sd if k.endswith("running_mean")}
 
     sf, sv = stats_of(m.frame_disc_model), stats_of(m.video_disc_model)
+    sf64 = {k: (a.clone(), b.clone()) for k, (a, b) in sf.items()}
+    sv64 = {k: (a.clone(), b.clone()) for k, (a, b) in sv.items()}
     data = inputs.step_batch(2, 128, 128)
+    m.frame_disc_model.plan_log, m.video_disc_model.plan_log = [], []
     ld = tr.step(data)
-    ref, new, newf, newv, _, grads = OS.gan_step(P, Pf, Pv, OL.synthetic_vgg19_state(), data, sf, sv)
+    torch.cuda.synchronize()
+    fl = [p.activation_signs() for p in m.frame_disc_model.plan_log]
+    vl = [p.activation_signs() for p in m.video_disc_model.plan_log]
+    m.frame_disc_model.plan_log = m.video_disc_model.plan_log = None
+    ref, new, newf, newv, _, _ = OS.gan_step(P, Pf, Pv, OL.synthetic_vgg19_state(), data, sf, sv)
     assert list(ld.keys()) == list(ref.keys()), (list(ld.keys()), list(ref.keys()))
     np.testing.assert_allclose([float(ld[k]) for k in ref], [ref[k] for k in ref], rtol=1e-4)
-
-    # Gradients: per-tensor relative L2 vs the fp32 oracle, median < 1e-3, worst < 3e-2
-    # (LeakyReLU kink flips, see test_disc_fp32_matches_oracle; BatchNorm-preceding conv
-    # biases, whose true gradient is 0, excluded).  Post-update weights: the first Adamax /
-    # Adam step moves each weight by ~lr*sign(grad), so a near-zero gradient element whose
-    # sign differs moves one weight by 2*lr: gate on the fraction of such elements.
-    bn_bias = {f"layer.{i}.bias" for i in (2, 5)}
-    for mod, g_ref, w_ref, tag in ((m.coarse_model, grads["g"], new, "g"), (m.frame_disc_model, grads["f"], newf, "f"),
-                                   (m.video_disc_model, grads["v"], newv, "v")):
+    _, _, _, _, _, g64 = OS.gan_step(P, Pf, Pv, OL.synthetic_vgg19_state(), data, sf64, sv64,
+                                     masks=m.coarse_model.last_plan.activation_signs(),
+                                     vmasks=tr.RGBLoss.vgg_loss.vgg_net.last_plan.activation_signs(),
+                                     gf_masks=fl[2], gv_masks=vl[2], df_masks=(fl[0], fl[1]), dv_masks=(vl[0], vl[1]),
+                                     dtype=torch.float64)
+    bn_bias = {f"layer.{i}.bias" for i in (2, 5)}  # conv biases before BatchNorm: true gradient 0
+    moved = total = 0
+    for mod, g_ref, w_ref, tag in ((m.coarse_model, g64["g"], new, "g"), (m.frame_disc_model, g64["f"], newf, "f"),
+                                   (m.video_disc_model, g64["v"], newv, "v")):
         named = dict(mod.named_parameters())
-        errs, moved, total = [], 0, 0
+        errs = {}
         for k, gr in g_ref.items():
             if tag != "g" and k in bn_bias:
+                assert float(named[k].grad.abs().max()) < 1e-4, k
                 continue
-            errs.append(rel_l2(named[k].grad, gr))
+            errs[k] = rel_l2(named[k].grad, gr)
             dw = (named[k].detach().cpu().double() - w_ref[k].double()).abs()
             moved += int((dw > 1e-4).sum())
             total += dw.numel()
-        assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (tag, float(np.median(errs)), max(errs))
-        assert moved <= 1e-3 * total, (tag, moved, total)
+        worst = max(errs, key=errs.get)
+        print(f"{tag}: {len(errs)} gradients vs fp64 oracle on the same branches: relative L2 median "
+              f"{np.median(list(errs.values())):.2e}, worst {errs[worst]:.2e} ({worst})")
+        assert errs[worst] <= 3e-4, (tag, worst, errs[worst])
+    assert moved <= 1e-3 * total, (moved, total)
 
 
-def test_intergan_vae_sn_two_steps(dev):
-    """The reference's InterGAN configuration: VAEHRNet coarse model (KLD term) with the SN
-    frame / video discriminators at 128x128, two fp32 steps: the second runs with SpectralNorm
-    u / v trainable after set_net_grad(True) (per-parameter Adam step counts); losses stay
-    finite, the KLD term sits after the CE term as in the reference (InterGANTrainer.py:406-409)
-    and u moves with the power iteration."""
+def _uv(k):
+    return k.endswith(("weight_u", "weight_v"))
+
+
+def _disc_oracle_params(mod, cls):
+    """the oracle's parameter set of a discriminator (u, v, weight_bar, bias; no running
+    statistics, no SpectralNorm effective-weight scratch) from the module's state"""
+    keys = set(OD.init_params(OD.SPECS[cls](23), 0))
+    sd = mod.state_dict()
+    return {k: sd[k].detach().cpu().clone() for k in keys if "running" not in k}
+
+
+def _opt_state(opt, named, kind):
+    """torch-format optimizer state -> oracle state (name -> dict); parameters without state
+    (SpectralNorm u / v before their first gradient) are absent"""
+    ids = {id(p): n for n, p in named.items()}
+    out = {}
+    for p, st in opt.state.items():
+        if id(p) not in ids or "step" not in st:
+            continue
+        step = int(float(st["step"]))
+        if kind == "adamax":
+            out[ids[id(p)]] = dict(step=step, exp_avg=st["exp_avg"].detach().cpu().clone(),
+                                   exp_inf=st["exp_inf"].detach().cpu().clone())
+        else:
+            out[ids[id(p)]] = dict(step=step, m=st["exp_avg"].detach().cpu().clone(),
+                                   v=st["exp_avg_sq"].detach().cpu().clone())
+    return out
+
+
+def _vae_zero_bias(sd_keys):
+    """VAE conv biases followed by train-mode BatchNorm (true gradient 0)"""
+    out = set()
+    for k in sd_keys:
+        if k.startswith("vae_") and k.endswith(".bias"):
+            pre, i = k[:-len(".bias")].rsplit(".", 1)
+            if f"{pre}.{int(i) + 1}.running_mean" in sd_keys:
+                out.add(k)
+    return out
+
+
+def test_intergan_vae_sn_steps_match_oracle(dev):
+    """The reference's own InterGAN configuration (VAEHRNet coarse model with the
+    KLD term, FrameSN / VideoSN discriminators, seg_disc, 128x128; InterGANNet.py:28-117,
+    InterGANTrainer.py:376-456, KLD losses.py:50-60, SpectralNorm.py:14-67) for two fp32 steps
+    against oracle.step.gan_step (pinned to the reference by G14, tests/test_oracle_gan.py).
+    Step 2 starts from this implementation's post-step-1 state (weights, u / v, BatchNorm
+    running statistics, optimizer states) with u / v trainable (set_net_grad(True)).  Per step:
+    * loss dict (KLD after CE, as the reference) within 1e-4 relative of the fp32 oracle;
+    * every gradient tensor -- generator (VAE encoder / decoder, mu / logvar FCs, HRNet trunk),
+      both discriminators, and the u / v gradients of step 2 -- against the fp64 oracle evaluated
+      on this step's activation branches (every LeakyReLU of every pass imposed): relative L2
+      <= 1e-4, <= 3e-4 for the VAE encoder / decoder / FC tensors (their gradient comes back
+      through train-mode BatchNorm backward, cancelling in fp32); BatchNorm-preceding conv
+      biases (true gradient 0) at rounding level of their layer's weight gradient;
+    * post-step weights within 1e-4 of the fp32 oracle's except a <= 1e-3 fraction (a first
+      Adam / Adamax step moves a weight by +-lr on the sign of a near-zero gradient), u / v
+      within 1e-5, running statistics within 1e-4."""
     os.environ["DVIE_PRECISION"] = "fp32"
     from deep_video_interpolation_extrapolation_amd.options import default_args
     from deep_video_interpolation_extrapolation_amd.runners.InterGANTrainer import InterGANTrainer
+    from oracle import vaehrnet as V
+    FR, VI = "FrameSNDiscriminator", "VideoSNDiscriminator"
     args = default_args("INTER", syn_type="inter", model="InterGANNet", gan=True, train_coarse=True, frame_disc=True,
                         video_disc=True, train_frame_disc=True, train_video_disc=True, seg_disc=True,
-                        coarse_model="VAEHRNet", vae=True, frame_disc_model="FrameSNDiscriminator",
-                        video_disc_model="VideoSNDiscriminator", batch_size=2, input_h=128, input_w=128,
-                        precision="fp32", synthetic=2, num_workers=0, split="train")
+                        coarse_model="VAEHRNet", vae=True, frame_disc_model=FR, video_disc_model=VI, batch_size=2,
+                        input_h=128, input_w=128, precision="fp32", synthetic=2, num_workers=0, split="train")
     torch.manual_seed(1024)
     tr = InterGANTrainer(args)
     m = tr.model.module
-    sn0 = m.frame_disc_model.layer[0].module
-    u0 = sn0.weight_u.detach().clone()
+    cm, fd, vd = m.coarse_model, m.frame_disc_model, m.video_disc_model
+    named = {"g": dict(cm.named_parameters()), "f": dict(fd.named_parameters()), "v": dict(vd.named_parameters())}
+    zero_b = _vae_zero_bias(set(cm.state_dict()))
     data = inputs.step_batch(2, 128, 128)
-    ld1 = tr.step(data)
-    assert sn0.weight_u.requires_grad  # set_net_grad(True) after the G pass, as the reference
-    ld2 = tr.step(data)
-    torch.cuda.synchronize()
-    keys = list(ld1.keys())
-    assert keys.index("coarse_kld_loss") == keys.index("coarse_ce_loss") + 1, keys
-    assert keys[-1] == "loss_all" and list(ld2.keys()) == keys
-    for ld in (ld1, ld2):
-        assert all(np.isfinite(float(v)) for v in ld.values()), ld
-    assert not torch.equal(sn0.weight_u.detach(), u0)
-    assert sn0.weight_u.grad is not None and bool(torch.isfinite(sn0.weight_u.grad).all())
+    vgg = OL.synthetic_vgg19_state()
+    state = None
+    for k in range(2):
+        Pg = {n: p.detach().cpu().clone() for n, p in named["g"].items()}
+        Pf, Pv = _disc_oracle_params(fd, FR), _disc_oracle_params(vd, VI)
+        vst = V.bn_stats({n: t.detach().cpu().clone() for n, t in cm.state_dict().items()})
+        if k > 0:
+            state = {"g": _opt_state(tr.coarse_opt, named["g"], "adamax"),
+                     "f": _opt_state(tr.frame_disc_opt, named["f"], "adam"),
+                     "v": _opt_state(tr.video_disc_opt, named["v"], "adam")}
+        fd.plan_log, vd.plan_log = [], []
+        ld = tr.step(data)
+        torch.cuda.synchronize()
+        assert all(p.requires_grad for p in fd.parameters())  # set_net_grad(True) after the G pass
+        eps = cm.last_eps.detach().cpu().clone()
+        masks = dict(cm.last_plan.activation_signs())
+        for r in (cm._enc, cm._dec):
+            masks.update(r.last_plan.activation_signs())
+        vmasks = tr.RGBLoss.vgg_loss.vgg_net.last_plan.activation_signs()
+        fl = [p.activation_signs() for p in fd.plan_log]
+        vl = [p.activation_signs() for p in vd.plan_log]
+        fd.plan_log = vd.plan_log = None
+        assert len(fl) == 3 and len(vl) == 3  # D(fake.detach()), D(real), frozen D(fake)
+        kw = dict(frame_spec=FR, video_spec=VI, uv_grad=k > 0)
+        ref, new, newf, newv, st32, _ = OS.gan_step(
+            Pg, Pf, Pv, vgg, data, {}, {}, vae={"eps": eps, "stats": {n: (a.clone(), b.clone()) for n, (a, b) in
+                                                                      vst.items()}},
+            state=None if state is None else {t: {n: dict(d) for n, d in s.items()} for t, s in state.items()}, **kw)
+        keys = list(ld.keys())
+        assert keys == list(ref.keys()), (keys, list(ref.keys()))
+        assert keys.index("coarse_kld_loss") == keys.index("coarse_ce_loss") + 1
+        np.testing.assert_allclose([float(ld[n]) for n in ref], [ref[n] for n in ref], rtol=1e-4)
+        _, _, _, _, _, g64 = OS.gan_step(
+            Pg, Pf, Pv, vgg, data, {}, {}, vae={"eps": eps, "stats": vst}, masks=masks, vmasks=vmasks,
+            gf_masks=fl[2], gv_masks=vl[2], df_masks=(fl[0], fl[1]), dv_masks=(vl[0], vl[1]),
+            dtype=torch.float64, **kw)
+        for tag in ("g", "f", "v"):
+            errs = {}
+            for n, gr in g64[tag].items():
+                got = named[tag][n].grad
+                assert got is not None, (k, tag, n)
+                if n in zero_b:
+                    w = named[tag][n[:-4] + "weight"].grad.double().norm()
+                    assert float(got.double().norm()) <= 1e-3 * float(w), (k, n)
+                    continue
+                errs[n] = rel_l2(got, gr)
+            if k == 0:  # u / v: no gradient in step 1 (requires_grad False until set_net_grad(True))
+                assert all(named[tag][n].grad is None for n in named[tag] if _uv(n)), tag
+            worst = max(errs, key=errs.get)
+            print(f"step {k + 1} {tag}: {len(errs)} gradients vs fp64 oracle on the same branches: relative L2 "
+                  f"median {np.median(list(errs.values())):.2e}, worst {errs[worst]:.2e} ({worst})")
+            for n, e in errs.items():
+                assert e <= (3e-4 if n.startswith(("vae_", "mu_fc", "logvar_fc")) else 1e-4), (k, tag, n, e)
+        if k > 0:
+            assert any(_uv(n) for n in g64["f"]) and any(_uv(n) for n in g64["v"])
+        moved = total = 0
+        for tag, ref_p in (("g", new), ("f", newf), ("v", newv)):
+            sd = {"g": cm, "f": fd, "v": vd}[tag].state_dict()
+            for n, w in ref_p.items():
+                if n in zero_b:
+                    continue
+                got = sd[n].detach().cpu().double()
+                if _uv(n):
+                    assert rel_l2(got, w) < 1e-5, (k, n)
+                    continue
+                d = (got - w.double()).abs()
+                moved += int((d > 1e-4).sum())
+                total += d.numel()
+        assert moved <= 1e-3 * total, (k, moved, total)
+        sd = cm.state_dict()
+        for n, (rm, rv) in st32["stats"][2].items():
+            pre, i = n.rsplit(".", 1)
+            assert rel_l2(sd[n + ".running_var"], rv) < 1e-4, (k, n)
+            if k > 0 and f"{pre}.{int(i) - 1}.bias" in zero_b:
+                continue  # the running mean carries step 1's +-lr noise move of the preceding conv bias
+            assert rel_l2(sd[n + ".running_mean"], rm) < 1e-4, (k, n)

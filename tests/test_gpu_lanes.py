@@ -1,11 +1,10 @@
 """GPU: the op-list executor's lanes (dvie_op.lane, include/dvie.h).
 
 The backward plans put every weight / bias gradient (WGRAD, WREDUCE, COLSUM ops) on the
-weight lane, and HRNet's resolution branches run as branch regions (one lane per branch,
-forward and backward).  Every kernel is deterministic, so the multi-stream run must be
-bit-identical to the one-stream run (DVIE_WGRAD_LANE=0 / DVIE_BRANCH_LANES=0 at plan
-compile time, or DVIE_OP_LANES=0 in the executor), over consecutive steps (the weight lane
-reuses the plan's weight-gradient workspace every step) and in fp32 and bf16."""
+weight lane.  Every kernel is deterministic, so the two-stream run must be bit-identical to
+the one-stream run (DVIE_WGRAD_LANE=0 at plan compile time, or DVIE_OP_LANES=0 in the
+executor), over consecutive steps (the weight lane reuses the plan's weight-gradient
+workspace every step) and in fp32 and bf16."""
 import pytest
 import torch
 
@@ -14,13 +13,12 @@ import inputs
 pytestmark = pytest.mark.gpu
 
 
-def _run_steps(dev, prec, monkeypatch, lane_env, op_lanes, branch="1", steps=2):
+def _run_steps(dev, prec, monkeypatch, lane_env, op_lanes, steps=2):
     import types
     from deep_video_interpolation_extrapolation_amd import nets
     monkeypatch.setenv("DVIE_PRECISION", prec)
     monkeypatch.setenv("DVIE_WGRAD_LANE", lane_env)
     monkeypatch.setenv("DVIE_OP_LANES", op_lanes)
-    monkeypatch.setenv("DVIE_BRANCH_LANES", branch)
     torch.manual_seed(1024)
     m = nets.InterNet(types.SimpleNamespace(syn_type="inter", highres_large=False, coarse_model="HRNet")).to(dev)
     x, seg = inputs.hrnet_input(2, 64, 128)
@@ -37,23 +35,20 @@ def _run_steps(dev, prec, monkeypatch, lane_env, op_lanes, branch="1", steps=2):
         out.append((rgb.detach().clone(), s.detach().clone(),
                     [p.grad.clone() for p in m.parameters() if p.grad is not None]))
     plan = m.coarse_model.last_plan
-    lanes = [sum(1 for i in range(plan.n_bwd) if plan.bwd_arr[i].lane == k) for k in range(8)]
-    lanes += [sum(1 for i in range(len(plan.fwd_arr)) if plan.fwd_arr[i].lane == k) for k in range(8)]
+    lanes = [sum(1 for i in range(plan.n_bwd) if plan.bwd_arr[i].lane == k) for k in range(2)]
+    lanes += [sum(1 for i in range(len(plan.fwd_arr)) if plan.fwd_arr[i].lane == k) for k in range(2)]
     return out, lanes
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_lanes_match_one_stream(dev, monkeypatch, prec):
     multi, n_multi = _run_steps(dev, prec, monkeypatch, "1", "1")
-    wlane, _ = _run_steps(dev, prec, monkeypatch, "1", "1", branch="0")
-    one, n_none = _run_steps(dev, prec, monkeypatch, "0", "1", branch="0")
+    one, n_none = _run_steps(dev, prec, monkeypatch, "0", "1")
     off, _ = _run_steps(dev, prec, monkeypatch, "1", "0")  # tagged, executor switch off
-    # weight lane in the backward, branch lanes 2 / 3 (stage 3's second and third branch)
-    # in both directions; nothing tagged without the switches
-    assert n_multi[1] > 50 and n_multi[2] >= 9 and n_multi[3] >= 8, n_multi
-    assert n_multi[8 + 2] > 5 and n_multi[8 + 3] > 5, n_multi
-    assert sum(n_none[k] for k in range(16) if k % 8) == 0, n_none
-    for ref, got in ((one, multi), (one, wlane), (one, off)):
+    # weight lane in the backward only; nothing tagged without the switch
+    assert n_multi[1] > 50 and n_multi[3] == 0, n_multi
+    assert n_none[1] == 0 and n_none[3] == 0, n_none
+    for ref, got in ((one, multi), (one, off)):
         for (ra, rb, rg), (ga, gb, gg) in zip(ref, got):
             assert torch.equal(ra, ga) and torch.equal(rb, gb)
             assert len(rg) == len(gg) and all(torch.equal(a, b) for a, b in zip(rg, gg))

@@ -152,7 +152,7 @@ def test_warp(dev):
 @pytest.mark.parametrize("with_dimg", [True, False])
 @pytest.mark.parametrize("shape,far_frac", [((2, 5, 40, 136), 0.05), ((1, 3, 33, 66), 0.05), ((2, 3, 70, 200), 0.0),
                                             ((1, 4, 37, 130), 0.002), ((2, 3, 36, 128), 0.05), ((1, 3, 20, 256), 0.0),
-                                            ((1, 3, 9, 64), 0.2)])
+                                            ((1, 3, 9, 64), 0.2), ((1, 3, 12, 1030), 0.0), ((2, 3, 16, 1024), 0.001)])
 def test_warp_multi_tile(dev, with_dimg, shape, far_frac):
     """dvie_warp_bwd through the C ABI on frames spanning many 256-pixel row segments: a
     smooth flow of a few pixels (every sample inside its corners' 3x3 pull windows) plus a
@@ -160,7 +160,9 @@ def test_warp_multi_tile(dev, with_dimg, shape, far_frac):
     reads from global memory, a tile without from its LDS-staged region: far_frac 0 and
     0.002 keep most tiles on the LDS path); the dimg + dflow path and the dflow-only path
     (dimg = NULL, no workspace); 3-5 channels.  Rows of a multiple of 64 pixels (whole
-    64-lane waves, no partial segment) are covered too.
+    64-lane waves, no partial segment) are covered too; 3 channels at even widths take the
+    two-pixels-per-lane forward (paired corner-row loads on smooth waves, one-pixel loads on
+    waves holding a far sample), 1030 a partial 512-pixel segment.
     Tolerances: out 1e-5, dimg 1e-4, dflow 1e-3 abs."""
     import ctypes
     from deep_video_interpolation_extrapolation_amd import _lib as L

@@ -143,14 +143,14 @@ def test_srn_refine_matches_oracle(dev, n_scales):
     gos = [torch.randn(o.shape, generator=g) for o in outs]
     sum((o * go.to(dev)).sum() for o, go in zip(outs, gos)).backward()
     torch.cuda.synchronize()
-    ref = OR.srn_forward(P, rgb, seg, enc, n_scales)
-    sum((o * go).sum() for o, go in zip(ref, gos)).backward()
+    # fp64 oracle on this run's LeakyReLU branches (Plan.activation_list, imposed in order)
+    P = {k: v.detach().double().requires_grad_(True) for k, v in P.items()}
+    ref = OR.srn_forward(P, rgb.double(), seg.double(), enc.double(), n_scales, masks=m.last_plan.activation_list())
+    sum((o * go.double()).sum() for o, go in zip(ref, gos)).backward()
     assert len(outs) == n_scales
     for o, r in zip(outs, ref):
-        assert o.shape == r.shape and float((o.detach().cpu() - r.detach()).abs().max()) < 1e-4
-    named = dict(m.named_parameters())
-    errs = [rel_l2(named[k].grad, P[k].grad) for k in P]
-    assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (float(np.median(errs)), max(errs))
+        assert o.shape == r.shape and float((o.detach().cpu().double() - r.detach()).abs().max()) < 1e-4
+    _check_tight(dict(m.named_parameters()), {k: v.grad for k, v in P.items()}, f"SRNRefine n_sc {n_scales}")
 
 
 @pytest.mark.parametrize("prop", [False, True])
@@ -168,14 +168,24 @@ def test_attn_refine_matches_oracle(dev, prop):
     gos = [torch.randn(o.shape, generator=g) for o in outs]
     sum((o * go.to(dev)).sum() for o, go in zip(outs, gos)).backward()
     torch.cuda.synchronize()
-    ref, rflows = OR.attn_forward(P, img, seg, x, nseg, 2, prop)
-    sum((o * go).sum() for o, go in zip(ref, gos)).backward()
+    P = {k: v.detach().double().requires_grad_(True) for k, v in P.items()}
+    ref, rflows = OR.attn_forward(P, img.double(), seg.double(), x.double(), nseg.double(), 2, prop,
+                                  masks=m.last_plan.activation_list())
+    sum((o * go.double()).sum() for o, go in zip(ref, gos)).backward()
     for o, r in zip(outs, ref):
-        assert float((o.detach().cpu() - r.detach()).abs().max()) < 1e-4
+        assert float((o.detach().cpu().double() - r.detach()).abs().max()) < 1e-4
     _check_flows(m, flows, rflows)
-    named = dict(m.named_parameters())
-    errs = [rel_l2(named[k].grad, P[k].grad) for k in P]
-    assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (float(np.median(errs)), max(errs))
+    _check_tight(dict(m.named_parameters()), {k: v.grad for k, v in P.items()}, f"MSResAttnRefine prop {prop}")
+
+
+def _check_tight(named, grads64, tag, bar=1e-4):
+    """every gradient tensor within `bar` relative L2 of the fp64 oracle evaluated on the HIP
+    run's activation branches (only fp32 rounding remains)"""
+    errs = {k: rel_l2(named[k].grad, g) for k, g in grads64.items()}
+    worst = max(errs, key=errs.get)
+    print(f"{tag}: {len(errs)} gradients vs fp64 oracle on the same branches: relative L2 median "
+          f"{np.median(list(errs.values())):.2e}, worst {errs[worst]:.2e} ({worst})")
+    assert errs[worst] <= bar, (tag, worst, errs[worst])
 
 
 def _check_flows(m, flows, rflows, tie=1e-4):
@@ -251,11 +261,13 @@ def test_two_stage_bf16_1024x2048(dev):
 
 
 @pytest.mark.timeout(300)
-def test_inter_trainer_stage3_step_matches_oracle(dev):
+def test_inter_trainer_stage3_step_matches_oracle(dev, monkeypatch):
     """InterTrainer --refine --stage3 (InterStage3Net, n_scales 2) fp32 step at 64x128 vs
     oracle.step.refine_step: loss dict (coarse, refine_<scale>, stage3_<scale> keys in the
-    reference order) within 1e-4; gradients of all three nets by per-tensor relative L2;
-    post-Adamax weights (fraction moved differently)."""
+    reference order) within 1e-4; every gradient tensor of all three nets within 1e-4 relative
+    L2 of the fp64 oracle on the step's branches (coarse HRNet, refine, stage-3 LeakyReLUs and
+    the ReLUs of every VGG-loss call imposed); post-Adamax weights (fraction moved differently)."""
+    from deep_video_interpolation_extrapolation_amd.nets.vgg import my_vgg
     from deep_video_interpolation_extrapolation_amd.runners.InterTrainer import InterTrainer
     from oracle import losses as OL
     from oracle import step as OS
@@ -264,18 +276,24 @@ def test_inter_trainer_stage3_step_matches_oracle(dev):
     torch.manual_seed(1024)
     tr = InterTrainer(a)
     data = OS.synthetic_batch(2, 64, 128)
+    monkeypatch.setattr(my_vgg, "sign_log", [])
     ld = tr.step(data)
+    vmasks = my_vgg.sign_log
     Pc = OH.init_params(1024)
     Pr = OR.init_params(None, OR.srn_specs())
     Ps = OR.init_params(None, OR.attn_specs())
-    ref, grads, new = OS.refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps)
+    ref, _, new = OS.refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps)
     assert list(ld.keys()) == list(ref.keys()), (list(ld.keys()), list(ref.keys()))
     np.testing.assert_allclose([float(ld[k]) for k in ref], [ref[k] for k in ref], rtol=1e-4)
     m = tr.model.module
+    assert len(vmasks) == 5  # coarse, refine x 2 scales, stage 3 x 2 scales
+    _, g64, _ = OS.refine_step(Pc, Pr, OL.synthetic_vgg19_state(), data, 2, Ps=Ps,
+                               masks=m.coarse_model.last_plan.activation_signs(),
+                               rmasks=m.refine_model.last_plan.activation_list(),
+                               smasks=m.stage3_model.last_plan.activation_list(), vmasks=vmasks, dtype=torch.float64)
     for part, mod in (("coarse", m.coarse_model), ("refine", m.refine_model), ("stage3", m.stage3_model)):
         named = dict(mod.named_parameters())
-        errs = [rel_l2(named[k].grad, g) for k, g in grads[part].items()]
-        assert float(np.median(errs)) < 1e-3 and max(errs) < 3e-2, (part, float(np.median(errs)), max(errs))
+        _check_tight(named, g64[part], f"InterStage3Net step {part}")
         moved = sum(int(((named[k].detach().cpu() - w).abs() > 1e-4).sum()) for k, w in new[part].items())
         total = sum(w.numel() for w in new[part].values())
         assert moved <= 1e-3 * total, (part, moved, total)

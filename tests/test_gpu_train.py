@@ -12,11 +12,11 @@ pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def trainer(prec, H, W, B):
+def trainer(prec, H, W, B, **kw):
     from deep_video_interpolation_extrapolation_amd.options import default_args
     from deep_video_interpolation_extrapolation_amd.runners.InterTrainer import InterTrainer
     args = default_args("INTER", syn_type="inter", train_coarse=True, batch_size=B, input_h=H, input_w=W,
-                        precision=prec, synthetic=B, num_workers=0, split="train")
+                        precision=prec, synthetic=B, num_workers=0, split="train", **kw)
     os.environ["DVIE_PRECISION"] = prec
     torch.manual_seed(1024)
     return InterTrainer(args)
@@ -61,9 +61,9 @@ def test_inter_step_matches_reference(dev):
     assert errs[worst] <= 1e-4, (worst, errs[worst])
 
 
-def _tape_step(prec, mode, data, monkeypatch):
+def _tape_step(prec, mode, data, monkeypatch, **kw):
     monkeypatch.setenv("DVIE_LOSS_TAPE", mode)
-    tr = trainer(prec, 64, 128, 2)
+    tr = trainer(prec, 64, 128, 2, **kw)
     ld = tr.forward_backward(data)
     named = dict(tr.model.module.coarse_model.named_parameters())
     return ({k: float(v) for k, v in ld.items()},
@@ -102,6 +102,23 @@ def test_loss_tape_matches_autograd_losses(dev, monkeypatch):
     ea, et = np.median(list(_rel(gab, ga).values())), np.median(list(_rel(gtb, ga).values()))
     print(f"bf16 gradients vs fp32: autograd form median {ea:.2e}, tape {et:.2e}")
     assert et <= 1.25 * ea + 1e-4, (et, ea)
+
+
+@pytest.mark.parametrize("zero", ["ssim_weight", "vgg_weight"])
+def test_loss_tape_zero_weight_term(dev, monkeypatch, zero):
+    """A loss term of weight 0 (--ssim_w 0 / --vgg_w 0) reports 0 in the loss dict and adds
+    nothing to loss_all, in the tape as in the autograd form and the reference
+    (losses.py:223-241 multiplies each term by its weight); gradients as the autograd form."""
+    data = inputs.step_batch(2, 64, 128)
+    la, ga = _tape_step("fp32", "0", data, monkeypatch, **{zero: 0.0})
+    lt, gt = _tape_step("fp32", "1", data, monkeypatch, **{zero: 0.0})
+    key = {"ssim_weight": "coarse_ssim_loss", "vgg_weight": "coarse_vgg_loss"}[zero]
+    assert la[key] == 0.0 and lt[key] == 0.0, (la[key], lt[key])
+    assert abs(lt["loss_all"] - sum(v for k, v in lt.items() if k != "loss_all")) <= 1e-6 * abs(lt["loss_all"])
+    for k in la:
+        assert abs(la[k] - lt[k]) <= 1e-6 * max(1.0, abs(la[k])), (k, la[k], lt[k])
+    errs = _rel(gt, ga)
+    assert max(errs.values()) <= 1e-5, max(errs.values())
 
 
 def test_adamax_matches_torch(dev):
@@ -225,3 +242,39 @@ def test_main_launcher_cycgen(dev, tmp_path):
             names = sorted(p.name for p in (out / sub / clip).iterdir())
             assert names == ["00.0.png", "01.0.png", "02.0.png"], (sub, clip, names)
             assert Image.open(out / sub / clip / "02.0.png").size == (64, 32)
+
+
+def test_capturable_split_decided_when_a_param_has_no_grad(dev):
+    """Capturable fused Adam (graph capture): a parameter without a gradient in the first
+    eager step after set_capturable (SpectralNorm u / v before set_net_grad(True)) still fixes
+    the group's 'step counts differ' decision on the host, so the captured step never reads
+    device step counts; the replayed updates equal torch 1.0.1 Adam with per-parameter counts."""
+    from deep_video_interpolation_extrapolation_amd.optim import Adam
+    from oracle import disc as OD
+    g = torch.Generator().manual_seed(5)
+    p0 = [torch.randn(6, generator=g), torch.randn(3, generator=g)]
+    ps = [t.clone().to(dev).requires_grad_(True) for t in p0]
+    opt = Adam(ps, lr=1e-3)
+    opt.set_capturable(True)
+    g1 = [torch.randn(6, generator=g), torch.randn(3, generator=g)]
+    ps[0].grad = g1[0].to(dev)  # ps[1] has no gradient: skipped, no state
+    opt.step()
+    assert opt._split == {0: True}
+    ps[1].grad = g1[1].to(dev)
+    opt.step()  # second eager step: ps[1] takes its first step here, outside the capture
+    torch.cuda.synchronize()
+    graph, side = torch.cuda.CUDAGraph(), torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph):
+            opt.step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+    P = {0: p0[0].clone(), 1: p0[1].clone()}
+    st = None
+    for grads in ({0: g1[0]}, {0: g1[0], 1: g1[1]}, {0: g1[0], 1: g1[1]}, {0: g1[0], 1: g1[1]}):
+        P, st = OD.adam_101(P, grads, 1e-3, st)
+    for i in range(2):
+        assert float((ps[i].detach().cpu() - P[i]).abs().max()) < 1e-6, i

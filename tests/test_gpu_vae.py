@@ -4,8 +4,9 @@ as 1x1 convs, the HIP reparameterisation and the HRNet trunk with the decoded fe
 its stem, against the fp64 oracle (oracle/vaehrnet.py, itself pinned to the reference by
 tests/golden/vaehrnet.npz) evaluated on the HIP run's LeakyReLU branches.
 
-Tolerances: outputs and mu / logvar 1e-5 relative L2; parameter gradients 2e-4 relative L2
-(BatchNorm-preceding conv biases: zero true gradient, compared absolutely)."""
+Tolerances: outputs and mu / logvar 1e-5 relative L2; parameter gradients 1e-4 relative L2
+(3e-4 through train-mode BatchNorm; BatchNorm-preceding conv biases: zero true gradient,
+compared absolutely)."""
 import os
 import types
 
@@ -32,7 +33,7 @@ def make(prec, dev):
 
 
 def masks_of(m):
-    out = {}
+    out = dict(m.last_plan.activation_signs())  # the HRNet trunk
     for r in (m._enc, m._dec):
         out.update(r.last_plan.activation_signs())
     return out
@@ -62,10 +63,14 @@ def test_vaehrnet_fp32_matches_oracle(dev):
             assert float(g.abs().max()) < 1e-4, k  # conv bias before BatchNorm: zero gradient
             continue
         errs[k] = rel_l2(g, v.grad)
-    # the trunk's LeakyReLU branches are not imposed on the oracle (HRNet has no masks
-    # hook), so a kink flip there moves some gradients: median and worst, as the HRNet tests
+    # every LeakyReLU branch (encoder, decoder, trunk) is imposed on the fp64 oracle: only fp32
+    # rounding remains.  1e-4 per tensor; 3e-4 for the encoder / decoder / FC tensors, whose
+    # gradient comes back through train-mode BatchNorm backward (cancelling in fp32)
     worst = max(errs, key=errs.get)
-    assert float(np.median(list(errs.values()))) < 1e-3 and errs[worst] < 3e-2, (worst, errs[worst])
+    print(f"VAEHRNet gradients vs fp64 oracle on the same branches: relative L2 median "
+          f"{np.median(list(errs.values())):.2e}, worst {errs[worst]:.2e} ({worst})")
+    for k, e in errs.items():
+        assert e <= (3e-4 if k.startswith(("vae_", "mu_fc", "logvar_fc")) else 1e-4), (k, e)
     sd = m.state_dict()
     for name, (rm, rv) in st.items():
         assert rel_l2(sd[name + ".running_mean"], rm) < 1e-5, name
