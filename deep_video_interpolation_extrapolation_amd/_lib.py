@@ -21,6 +21,7 @@ EW_FUSE, EW_UPT, EW_POOL, EW_POOLT, EW_COPY, EW_L1SIGN, EW_NCHW, EW_TONCHW, EW_M
 LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC, LOSS_COSNHWC, LOSS_IOU, LOSS_ARGMAX_IOU = range(9)
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
 OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD, OP_ATTN, OP_HEAD3_BWD, OP_SEGENC_FWD = 8, 9, 10, 11, 12, 13, 14
+OP_SEGENC_BWD = 15
 (ATTN_L2NORM, ATTN_L2NORM_BWD, ATTN_CORR, ATTN_GATHER, ATTN_GATHER_T, ATTN_SOFTMAX, ATTN_SOFTMAX_BWD, ATTN_WNORM,
  ATTN_WNORM_BWD, ATTN_POOL, ATTN_POOL_T) = range(11)
 
@@ -197,11 +198,20 @@ class SegencDesc(ctypes.Structure):
     ]
 
 
+class SegencBwdDesc(ctypes.Structure):
+    _fields_ = [
+        ("dout", vp), ("e2", vp), ("e1", vp), ("inp", vp), ("w4d", vp), ("w2d", vp),
+        ("dw4", vp), ("dw2", vp), ("dw0", vp), ("db4", vp), ("db2", vp), ("db0", vp),
+        ("dout_ld", i64), ("e2_ld", i64), ("e1_ld", i64), ("in_ld", i64),
+        ("n", i32), ("h", i32), ("w", i32), ("kpad4", i32), ("kpad2", i32), ("slabs", i32),
+    ]
+
+
 class _OpUnion(ctypes.Union):
     _fields_ = [
         ("conv", ConvDesc), ("wgrad", WgradDesc), ("wreduce", WreduceDesc), ("colsum", ColsumDesc),
         ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList), ("bn", BnDesc), ("head", HeadDesc),
-        ("attn", AttnDesc), ("head3", Head3BwdDesc), ("segenc", SegencDesc),
+        ("attn", AttnDesc), ("head3", Head3BwdDesc), ("segenc", SegencDesc), ("segenc_bwd", SegencBwdDesc),
     ]
 
 
@@ -211,7 +221,7 @@ class Op(ctypes.Structure):
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
-        OP_ATTN: AttnDesc, OP_HEAD3_BWD: Head3BwdDesc, OP_SEGENC_FWD: SegencDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
+        OP_ATTN: AttnDesc, OP_HEAD3_BWD: Head3BwdDesc, OP_SEGENC_FWD: SegencDesc, OP_SEGENC_BWD: SegencBwdDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
 
 EXPORTS = [
     "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
@@ -221,7 +231,7 @@ EXPORTS = [
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
     "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs", "dvie_head3_bwd",
-    "dvie_segenc_fwd",
+    "dvie_segenc_fwd", "dvie_segenc_bwd",
 ]
 
 _lib = None
@@ -256,7 +266,7 @@ def load():
         for name in ("dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_reduce", "dvie_colsum", "dvie_ew",
                      "dvie_loss", "dvie_warp_fwd", "dvie_warp_bwd", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_head_fwd",
                      "dvie_head_bwd", "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_clip_prep", "dvie_attn",
-                     "dvie_head3_bwd", "dvie_segenc_fwd"):
+                     "dvie_head3_bwd", "dvie_segenc_fwd", "dvie_segenc_bwd"):
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]

@@ -16,6 +16,8 @@
 // others read a clamped row and are discarded), B = the source image at the tap's shift
 // (8 consecutive channels of one pixel per lane).  Epilogue: permlane32 pairing gives a lane 8
 // consecutive channels of one pixel, + bias, ELU, bf16.
+#include <algorithm>
+
 #include "common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -224,5 +226,356 @@ extern "C" int dvie_segenc_fwd(const dvie_segenc_desc* d, void* stream) {
   DVIE_CHECK_ARG(nt < (1LL << 30), "segenc: too many tiles");
   const int grid = (int)(nt < 256 ? nt : 256);  // one 147-KB workgroup per CU, tiles round-robin
   hipLaunchKernelGGL(segenc_fwd_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y, (int)nt);
+  DVIE_RETURN_LAUNCH();
+}
+
+// ============================================================================================
+// Fused backward of the segmentation encoder (the three convs above; the encoder input needs
+// no gradient).  Per 4 x 64 tile, with dout = the gradient of the encoder output:
+//   d_e2 = ELU'(e2) * conv4^T(dout)   on the 6 x 66 region the next step needs (zero outside
+//                                     the image),
+//   d_e1 = ELU'(e1) * conv2^T(d_e2)   on the tile,
+//   dW4 += dout^T (x) e2,  dW2 += d_e2^T (x) e1,  dW0 += d_e1^T (x) in   (3x3 shifts, K = pixels),
+//   db4 / db2 / db0 += column sums of dout / d_e2 / d_e1.
+// Nothing but the weight-gradient partial slabs leaves the kernel: d_e2 and d_e1 live in
+// LDS.  A workgroup walks tiles round-robin and keeps its 25 weight-gradient accumulator
+// tiles (32 x 32) in registers; it writes one slab per weight (dvie_conv2d_wgrad layout,
+// part[slab][o][t * cin + ci]) and per bias at the end.
+// LDS images: dout [8 x 68 px][16 B]; e2, d_e2, e1 [6 x 66 px][64 B] and d_e1 [4 x 64][64 B]
+// with 16-B chunk c of pixel p at (c ^ ((p >> 2) & 3)) (conflict-free row and transposed
+// reads); in [6 x 66][48 B].  The conv-transpose products read A = packed data-gradient
+// weights, B = the source image at the tap's shift (as the forward); the weight gradients
+// read A = the output-gradient image and B = the input image at the tap's shift, both with
+// ds_read_b64_tr_b16 transposed reads.
+namespace dvie {
+
+__device__ __forceinline__ bf16x8 hb_tr_pair_se(const char* p0, const char* p1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)p0);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)p1);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct SbCfg {
+  static constexpr int NW = 8, R = 4, TW = 64;
+  static constexpr int DO_W = TW + 4, DO_H = R + 4;  // origin (-2, -2)
+  static constexpr int E_W = TW + 2, E_H = R + 2;    // origin (-1, -1)
+  static constexpr int DO_PC = (DO_H * DO_W + 63) / 64;
+  static constexpr int E_PC = (E_H * E_W * 4 + 63) / 64;
+  static constexpr int IN_PC = (E_H * E_W * 3 + 63) / 64;
+  static constexpr int W4_PITCH = 5 * 32 + 16, W2_PITCH = 18 * 32 + 16;
+  static constexpr int O_DO = 0, O_E2 = O_DO + DO_PC * 1024, O_E1 = O_E2 + E_PC * 1024, O_IN = O_E1 + E_PC * 1024;
+  static constexpr int O_D2 = O_IN + IN_PC * 1024, O_D1 = O_D2 + E_H * E_W * 64, O_W4 = O_D1 + R * TW * 64;
+  static constexpr int O_W2 = O_W4 + 32 * W4_PITCH, O_RED = O_W2 + 32 * W2_PITCH;
+  static constexpr int SMEM = O_RED + 8 * 72 * 4;
+  static constexpr int PCS = DO_PC + 2 * E_PC + IN_PC;  // DMA pieces per tile
+  static constexpr int PQ = (PCS + NW - 1) / NW;
+};
+static_assert(SbCfg::SMEM <= 163840, "segenc backward LDS");
+
+// byte offset of 16-B chunk c of pixel p in a swizzled 64-B-pitch image
+__device__ __forceinline__ int sw64(int p, int c) { return p * 64 + ((c ^ ((p >> 2) & 3)) << 4); }
+
+__global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_desc p, int tiles_x, int tiles_y,
+                                                         int n_tiles) {
+  typedef SbCfg C;
+  constexpr int NW = C::NW;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int g4 = lane >> 4, li = lane & 15, qq = li >> 2, pq = li & 3;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // ---- data-gradient weights into LDS, once: w4d [32 ci][80 k], w2d [32 ci][288 k] ----
+  for (int i = tid; i < 32 * 10; i += NW * 64) {
+    const int r = i / 10, ch = i - r * 10;
+    *(i32x4*)(smem + C::O_W4 + r * C::W4_PITCH + ch * 16) = *(const i32x4*)((const bf16_t*)p.w4d + r * p.kpad4 + ch * 8);
+  }
+  for (int i = tid; i < 32 * 36; i += NW * 64) {
+    const int r = i / 36, ch = i - r * 36;
+    *(i32x4*)(smem + C::O_W2 + r * C::W2_PITCH + ch * 16) = *(const i32x4*)((const bf16_t*)p.w2d + r * p.kpad2 + ch * 8);
+  }
+
+  // ---- DMA geometry: piece -> (image, slot) ----
+  // images: 0 dout (1 chunk / px, origin -2), 1 e2 / 2 e1 (4 chunks, swizzled, origin -1), 3 in (3 chunks)
+  int geo[C::PQ];
+#pragma unroll
+  for (int q = 0; q < C::PQ; ++q) {
+    const int pc = wave + NW * q;
+    int v = -1;
+    if (pc < C::DO_PC) {
+      const int px = pc * 64 + lane;
+      if (px < C::DO_H * C::DO_W) v = (0 << 28) | ((px / C::DO_W) << 20) | ((px % C::DO_W) << 8);
+    } else if (pc < C::DO_PC + 2 * C::E_PC) {
+      const int img = pc < C::DO_PC + C::E_PC ? 1 : 2;
+      const int slot = (pc - C::DO_PC - (img - 1) * C::E_PC) * 64 + lane, px = slot >> 2;
+      const int src = (slot & 3) ^ ((px >> 2) & 3);
+      if (px < C::E_H * C::E_W) v = (img << 28) | ((px / C::E_W) << 20) | ((px % C::E_W) << 8) | src;
+    } else if (pc < C::PCS) {
+      const int slot = (pc - C::DO_PC - 2 * C::E_PC) * 64 + lane, px = slot / 3;
+      if (px < C::E_H * C::E_W) v = (3 << 28) | ((px / C::E_W) << 20) | ((px % C::E_W) << 8) | (slot - 3 * px);
+    }
+    geo[q] = v;
+  }
+  const unsigned long long npx = (unsigned long long)p.n * p.h * p.w;
+  const __amdgpu_buffer_rsrc_t rs[4] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dout, 0, (int)((npx - 1) * p.dout_ld * 2ull + 16ull), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.e2, 0, (int)((npx - 1) * p.e2_ld * 2ull + 64ull), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.e1, 0, (int)((npx - 1) * p.e1_ld * 2ull + 64ull), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.in, 0, (int)((npx - 1) * p.in_ld * 2ull + 48ull), 0x00020000)};
+  const unsigned rows[4] = {(unsigned)p.dout_ld * 2u, (unsigned)p.e2_ld * 2u, (unsigned)p.e1_ld * 2u,
+                            (unsigned)p.in_ld * 2u};
+
+  // ---- weight-gradient accumulator tiles of this wave: (gemm, first N block, count) ----
+  // waves 0-2: dW4 (M = 8 rows of 32, N = 288 = 9 blocks), 3-5: dW2 (9 blocks), 6-7: dW0 (7)
+  const int gemm = wave < 3 ? 0 : wave < 6 ? 1 : 2;
+  const int nb0 = gemm < 2 ? 3 * (wave - 3 * gemm) : (wave == 6 ? 0 : 4);
+  const int nbn = gemm < 2 ? 3 : (wave == 6 ? 4 : 3);
+  const int cin = gemm == 2 ? 24 : 32;
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  float bsum = 0.f;  // bias partial: thread tid < 504 owns channel tid % 72, pixels tid / 72 + 7 k
+
+  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    int tt = t;
+    const int x0 = (tt % tiles_x) * C::TW;
+    tt /= tiles_x;
+    const int y0 = (tt % tiles_y) * C::R;
+    const int n = tt / tiles_y;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < C::PQ; ++q) {
+      const int pc = wave + NW * q;
+      if (pc >= C::PCS) continue;  // (wave-uniform)
+      const int v = geo[q];
+      // (image from the piece index: the LDS destination must be wave-uniform)
+      const int img = pc < C::DO_PC ? 0 : pc < C::DO_PC + C::E_PC ? 1 : pc < C::DO_PC + 2 * C::E_PC ? 2 : 3;
+      const int org = img == 0 ? 2 : 1;
+      const int iy = y0 - org + ((v >> 20) & 0xFF), ix = x0 - org + ((v >> 8) & 0xFFF);
+      const bool ok = v >= 0 && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
+      const unsigned o = ok ? (unsigned)((n * p.h + iy) * p.w + ix) * rows[img] + (unsigned)(v & 15) * 16u : OOB;
+      int dst = img == 0 ? C::O_DO + pc * 1024
+                         : img == 1 ? C::O_E2 + (pc - C::DO_PC) * 1024
+                                    : img == 2 ? C::O_E1 + (pc - C::DO_PC - C::E_PC) * 1024
+                                               : C::O_IN + (pc - C::DO_PC - 2 * C::E_PC) * 1024;
+      __amdgpu_buffer_rsrc_t r = img == 0 ? rs[0] : img == 1 ? rs[1] : img == 2 ? rs[2] : rs[3];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_se)(smem + dst), 16, o, 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+
+    // ---- phase 1: d_e2 on the 6 x 66 region = ELU'(e2) * conv4^T(dout) ----
+    for (int blk = wave; blk < (C::E_H * C::E_W + 31) / 32; blk += NW) {
+      const int q = blk * 32 + r32;
+      const int qc = q < C::E_H * C::E_W ? q : C::E_H * C::E_W - 1;
+      const int rr = qc / C::E_W, cc = qc - rr * C::E_W;
+      const char* B = smem + C::O_DO + (rr * C::DO_W + cc) * 16;
+      f32x16 a1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        const i32x4 a = *(const i32x4*)(smem + C::O_W4 + r32 * C::W4_PITCH + hh * 16 + s * 32);
+        int kc = 2 * s + hh;
+        kc = kc < 9 ? kc : 8;
+        const i32x4 b = *(const i32x4*)(B + ((kc / 3) * C::DO_W + kc % 3) * 16);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1, 0,
+                                                     0, 0);
+      }
+      const int gy = y0 - 1 + rr, gx = x0 - 1 + cc;
+      const bool in = q < C::E_H * C::E_W && (unsigned)gy < (unsigned)p.h && (unsigned)gx < (unsigned)p.w;
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1[8 * P + e]),
+                                                           __float_as_uint(a1[8 * P + 4 + e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+        const int ch = 2 * P + hh;  // 16-B chunk: channels 8 ch .. +7
+        const i32x4 z = *(const i32x4*)(smem + C::O_E2 + sw64(qc, ch));
+        i32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float za = __uint_as_float(((uint32_t)z[e]) << 16), zb = __uint_as_float(((uint32_t)z[e]) & 0xffff0000u);
+          o[e] = (int)se_pack(in ? v[2 * e] * act_dz(za, DVIE_ACT_ELU, 0.f) : 0.f,
+                              in ? v[2 * e + 1] * act_dz(zb, DVIE_ACT_ELU, 0.f) : 0.f);
+        }
+        if (q < C::E_H * C::E_W) *(i32x4*)(smem + C::O_D2 + sw64(q, ch)) = o;
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 2: d_e1 on the tile = ELU'(e1) * conv2^T(d_e2) ----
+    {
+      const int blk = wave;  // 8 blocks of 32 pixels
+      const int q = blk * 32 + r32, rr = q >> 6, cc = q & 63;
+      f32x16 a1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 18; ++s) {
+        const i32x4 a = *(const i32x4*)(smem + C::O_W2 + r32 * C::W2_PITCH + hh * 16 + s * 32);
+        const int kc = 2 * s + hh, tp = kc >> 2, ck = kc & 3;
+        const int pe = (rr + tp / 3) * C::E_W + cc + tp % 3;
+        const i32x4 b = *(const i32x4*)(smem + C::O_D2 + sw64(pe, ck));
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1, 0,
+                                                     0, 0);
+      }
+      const int gy = y0 + rr, gx = x0 + cc;
+      const bool in = gy < p.h && gx < p.w;
+      const int pe = (rr + 1) * C::E_W + cc + 1;
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1[8 * P + e]),
+                                                           __float_as_uint(a1[8 * P + 4 + e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+        const int ch = 2 * P + hh;
+        const i32x4 z = *(const i32x4*)(smem + C::O_E1 + sw64(pe, ch));
+        i32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float za = __uint_as_float(((uint32_t)z[e]) << 16), zb = __uint_as_float(((uint32_t)z[e]) & 0xffff0000u);
+          o[e] = (int)se_pack(in ? v[2 * e] * act_dz(za, DVIE_ACT_ELU, 0.f) : 0.f,
+                              in ? v[2 * e + 1] * act_dz(zb, DVIE_ACT_ELU, 0.f) : 0.f);
+        }
+        *(i32x4*)(smem + C::O_D1 + sw64(q, ch)) = o;
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 3: weight gradients over the tile's 256 pixels (K = pixels) ----
+    // A = output-gradient image (rows o, 8 consecutive pixels per lane via two transposed
+    // reads), B = input image at the tap's shift (columns n = t * cin + ci)
+#pragma unroll 1
+    for (int sl = 0; sl < 16; ++sl) {
+      const int P0 = 16 * sl + 8 * (g4 >> 1) + qq;  // lane's tile pixel (+ 4 for the second read)
+      const int rr = P0 >> 6, cc = P0 & 63;
+      bf16x8 av;
+      if (gemm == 0) {  // dout rows o = 16 (g4 & 1) + 4 pq .. +3: rows past 7 read finite neighbours
+        const int o0 = (16 * (g4 & 1) + 4 * pq) & 7;
+        const char* a0 = smem + C::O_DO + ((rr + 2) * C::DO_W + cc + 2) * 16 + o0 * 2;
+        av = hb_tr_pair_se(a0, a0 + 4 * 16);
+      } else if (gemm == 1) {
+        const int o0 = 16 * (g4 & 1) + 4 * pq, pe = (rr + 1) * C::E_W + cc + 1;
+        const char* a0 = smem + C::O_D2 + sw64(pe, o0 >> 3) + (o0 & 7) * 2;
+        const char* a1 = smem + C::O_D2 + sw64(pe + 4, o0 >> 3) + (o0 & 7) * 2;
+        av = hb_tr_pair_se(a0, a1);
+      } else {
+        const int o0 = 16 * (g4 & 1) + 4 * pq;
+        const char* a0 = smem + C::O_D1 + sw64(P0, o0 >> 3) + (o0 & 7) * 2;
+        const char* a1 = smem + C::O_D1 + sw64(P0 + 4, o0 >> 3) + (o0 & 7) * 2;
+        av = hb_tr_pair_se(a0, a1);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= nbn) break;  // (wave-uniform)
+        const int n0 = 32 * (nb0 + j) + 16 * (g4 & 1) + 4 * pq;
+        int tp = n0 / cin;
+        const int ci = n0 - tp * cin;
+        tp = tp < 9 ? tp : 8;  // columns past 9 cin: finite data, discarded
+        const int pe = (rr + tp / 3) * C::E_W + cc + tp % 3;
+        const char *b0, *b1;
+        if (gemm == 2) {
+          b0 = smem + C::O_IN + pe * 48 + ci * 2;
+          b1 = b0 + 4 * 48;
+        } else {
+          const int base = gemm == 0 ? C::O_E2 : C::O_E1;
+          b0 = smem + base + sw64(pe, ci >> 3) + (ci & 7) * 2;
+          b1 = smem + base + sw64(pe + 4, ci >> 3) + (ci & 7) * 2;
+        }
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, hb_tr_pair_se(b0, b1), acc[j], 0, 0, 0);
+      }
+    }
+    // ---- bias column sums (dout 8, d_e2 32, d_e1 32 channels over the tile) ----
+    if (tid < 504) {
+      const int ch = tid % 72, part = tid / 72;
+      for (int px = part; px < 256; px += 7) {
+        const int rr = px >> 6, cc = px & 63;
+        const char* a;
+        int c;
+        if (ch < 8) {
+          a = smem + C::O_DO + ((rr + 2) * C::DO_W + cc + 2) * 16;
+          c = ch;
+        } else if (ch < 40) {
+          c = ch - 8;
+          a = smem + C::O_D2 + sw64((rr + 1) * C::E_W + cc + 1, c >> 3);
+          c &= 7;
+        } else {
+          c = ch - 40;
+          a = smem + C::O_D1 + sw64(px, c >> 3);
+          c &= 7;
+        }
+        bsum += bf2f(*(const bf16_t*)(a + c * 2));
+      }
+    }
+  }
+
+  // ---- this workgroup's slabs ----
+  const int slab = blockIdx.x;
+  {
+    float* out = gemm == 0 ? p.dw4 : gemm == 1 ? p.dw2 : p.dw0;
+    const int cout = gemm == 0 ? 8 : 32, kw = 9 * cin;
+    out += (long long)slab * cout * kw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j >= nbn) break;
+      const int n = 32 * (nb0 + j) + r32;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int o = 8 * i + 4 * hh + e;
+          if (o < cout && n < kw) out[o * kw + n] = acc[j][4 * i + e];
+        }
+    }
+  }
+  float* red = (float*)(smem + C::O_RED);
+  __syncthreads();
+  if (tid < 504) red[tid] = bsum;
+  __syncthreads();
+  if (tid < 72) {
+    float s = 0.f;
+    for (int k = 0; k < 7; ++k) s += red[k * 72 + tid];
+    if (tid < 8)
+      p.db4[slab * 8 + tid] = s;
+    else if (tid < 40)
+      p.db2[slab * 32 + tid - 8] = s;
+    else
+      p.db0[slab * 32 + tid - 40] = s;
+  }
+}
+
+}  // namespace dvie
+
+extern "C" int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream) {
+  using namespace dvie;
+  DVIE_CHECK_ARG(d && d->dout && d->e2 && d->e1 && d->in && d->w4d && d->w2d, "segenc_bwd: null pointer");
+  DVIE_CHECK_ARG(d->dw4 && d->dw2 && d->dw0 && d->db4 && d->db2 && d->db0, "segenc_bwd: null slab");
+  DVIE_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->slabs > 0, "segenc_bwd: shape");
+  DVIE_CHECK_ARG(d->dout_ld >= 8 && d->e2_ld >= 32 && d->e1_ld >= 32 && d->in_ld >= 24, "segenc_bwd: leading dims");
+  DVIE_CHECK_ARG(d->kpad4 >= 80 && d->kpad2 >= 288, "segenc_bwd: kpad");
+  const unsigned long long npx = (unsigned long long)d->n * d->h * d->w;
+  const long long ld = std::max(std::max(d->dout_ld, d->e2_ld), std::max(d->e1_ld, d->in_ld));
+  DVIE_CHECK_ARG(npx * (unsigned long long)ld * 2ull < 0xFFFFFF00ull && npx < (1ull << 31),
+                 "segenc_bwd: maps exceed the 32-bit buffer range");
+  const int tiles_x = (d->w + 63) / 64, tiles_y = (d->h + 3) / 4;
+  const long long nt = (long long)tiles_x * tiles_y * d->n;
+  DVIE_CHECK_ARG(nt < (1LL << 30), "segenc_bwd: too many tiles");
+  hipLaunchKernelGGL(segenc_bwd_kernel, dim3(d->slabs), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y,
+                     (int)nt);
   DVIE_RETURN_LAUNCH();
 }

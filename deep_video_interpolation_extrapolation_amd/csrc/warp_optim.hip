@@ -850,6 +850,7 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
       case DVIE_OP_ATTN: rc = dvie_attn(&o.u.attn, s); break;
       case DVIE_OP_HEAD3_BWD: rc = dvie_head3_bwd(&o.u.head3, s); break;
       case DVIE_OP_SEGENC_FWD: rc = dvie_segenc_fwd(&o.u.segenc, s); break;
+      case DVIE_OP_SEGENC_BWD: rc = dvie_segenc_bwd(&o.u.segenc_bwd, s); break;
       default: set_error("run_ops: unknown op kind %d at %d", o.kind, i); return finish(DVIE_EINVAL);
     }
     if (rc != DVIE_OK) {
@@ -880,6 +881,7 @@ size_t dvie_abi_sizeof(int which) {
     case DVIE_OP_ATTN: return sizeof(dvie_attn_desc);
     case DVIE_OP_HEAD3_BWD: return sizeof(dvie_head3_bwd_desc);
     case DVIE_OP_SEGENC_FWD: return sizeof(dvie_segenc_desc);
+    case DVIE_OP_SEGENC_BWD: return sizeof(dvie_segenc_bwd_desc);
     case 100: return sizeof(dvie_warp_desc);
     case 101: return sizeof(dvie_softmax_desc);
     case 102: return sizeof(dvie_sn_layer);

@@ -1094,9 +1094,87 @@ class Plan:
         self.bwd.append(self.ew_desc(L.EW_COPY, self.nb, out.H, out.W, out.c, gp, b.C, [(gp, b.C, out.H, out.W)],
                                      z=self.ptr(out), z_ld=b.C, dact=op.act))
 
+    def _segenc_bwd_chains(self):
+        """id(last op) -> chain for the segmentation encoders whose backward runs as one
+        dvie_segenc_bwd launch: the forward is fusable, the encoder input needs no gradient and
+        the intermediates have no other reader."""
+        out = {}
+        if os.environ.get("DVIE_SEGENC_FUSED", "1") == "0":
+            return out
+        for chain in getattr(self.g, "segenc", []):
+            o0, o1, o2 = chain
+            if not self._segenc_fusable(chain) or o0.x.buf.needs_grad:
+                continue
+            if not all(op.layer.trainable for op in chain):
+                continue
+            if len(o0.out.buf.consumers) != 1 or len(o1.out.buf.consumers) != 1:
+                continue
+            if self.nb * o0.x.H * o0.x.W * max(o2.out.buf.C, 32) * 2 >= 0xFFFFFF00:
+                continue
+            out[id(o2)] = chain
+        return out
+
+    def _segenc_backward(self, chain, gout, gld):
+        """dvie_segenc_bwd (all three weight / bias gradients of one encoder, d_e2 and d_e1 on
+        chip) into this chain's own slab buffers, then the slab reductions on the weight lane."""
+        o0, o1, o2 = chain
+        x, nb = o0.x, self.nb
+        slabs = 256
+        bufs = {k: torch.empty(slabs * n, dtype=torch.float32, device=self.device) for k, n in
+                (("dw4", 8 * 288), ("dw2", 32 * 288), ("dw0", 32 * 216), ("db4", 8), ("db2", 32), ("db0", 32))}
+        self.keep += list(bufs.values())
+        (_, w4d, kpad4), = self._dgrad_weights(o2.layer, x.H, x.W)
+        (_, w2d, kpad2), = self._dgrad_weights(o1.layer, x.H, x.W)
+        o = self._op(L.OP_SEGENC_BWD)
+        d = o.u.segenc_bwd
+        d.dout, d.e2, d.e1, d.inp = gout, self.ptr(o1.out), self.ptr(o0.out), self.ptr(x)
+        d.dout_ld, d.e2_ld, d.e1_ld, d.in_ld = gld, o1.out.buf.C, o0.out.buf.C, x.buf.C
+        d.w4d, d.w2d, d.kpad4, d.kpad2 = w4d.data_ptr(), w2d.data_ptr(), kpad4, kpad2
+        for k in ("dw4", "dw2", "dw0", "db4", "db2", "db0"):
+            setattr(d, k, bufs[k].data_ptr())
+        d.n, d.h, d.w, d.slabs = nb, x.H, x.W, slabs
+        npx = nb * x.H * x.W
+        o.meta = dict(cls="conv_wgrad", name="seg_encoder (fused backward)",
+                      flops=2.0 * npx * 9 * (2 * o2.layer.cout * o2.layer.cin + 2 * o1.layer.cout * o1.layer.cin
+                                             + o0.layer.cout * o0.layer.cin),
+                      bytes=float(self.es * npx * (8 + 32 + 32 + x.c)))
+        self.bwd.append(o)
+        for op, wk, bk in ((o2, "dw4", "db4"), (o1, "dw2", "db2"), (o0, "dw0", "db0")):
+            lay, xin = op.layer, op.x
+            first = lay not in self.wg_first
+            r_op = self._op(L.OP_WREDUCE)
+            r = r_op.u.wreduce
+            r.ws, r.dw, r.cmap = bufs[wk].data_ptr(), 0, lay.cmap_t.data_ptr()
+            r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, 9 * xin.c, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, xin.c
+            r.beta = 0 if first else 1
+            r_op.ws_ptr = bufs[wk].data_ptr()
+            r_op.meta = _reduce_meta(lay.name, r)
+            self.bwd.append(r_op)
+            self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
+            b_op = self._op(L.OP_WREDUCE)
+            r = b_op.u.wreduce
+            r.ws, r.dw, r.cmap = bufs[bk].data_ptr(), 0, None
+            r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, 1, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
+            r.beta = 0 if first else 1
+            b_op.ws_ptr = bufs[bk].data_ptr()
+            b_op.meta = _reduce_meta(lay.name + ".bias", r)
+            self.bwd.append(b_op)
+            self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
+            self.wg_first[lay] = True
+            self._uses_left[lay] -= 1
+            if self._uses_left[lay] == 0:
+                self.completions.append((len(self.bwd), lay))
+        for op in (o0, o1):  # their output gradients are never formed (d_e1 / d_e2 stay on chip)
+            op.out.buf.done = True
+            op.out.buf.pending = {}
+
     def _build_backward(self):
         g = self.g
         nb = self.nb
+        seg_bwd = self._segenc_bwd_chains()
+        seg_skip = {id(op) for ch in seg_bwd.values() for op in ch[:2]}
         self.wg_first = {}
         self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
         self._uses_left = {}
@@ -1165,6 +1243,11 @@ class Plan:
                         o.u.ew.std = op.std_t.data_ptr()
                     self.ext_grad.setdefault(op.key, []).append((len(self.bwd), op))
                     self.bwd.append(o)
+                continue
+            if id(op) in seg_bwd:
+                self._segenc_backward(seg_bwd[id(op)], gout, gld)
+                continue
+            if id(op) in seg_skip:
                 continue
             if isinstance(op, ConvOp):
                 self._conv_backward(op, gout, gld)

@@ -604,6 +604,36 @@ typedef struct dvie_segenc_desc {
 int dvie_segenc_fwd(const dvie_segenc_desc* d, void* stream);
 
 /*
+ * Fused backward of the same encoder (the encoder input needs no gradient): from dout (the
+ * gradient of the 8-channel output, bf16 NHWC, e.g. a slice of the stem buffer's gradient)
+ * and the forward's e2 / e1 / in, the weight- and bias-gradient partial slabs of the three
+ * convs; d_e2 = ELU'(e2) conv4^T(dout) and d_e1 = ELU'(e1) conv2^T(d_e2) stay on chip.
+ * w4d / w2d: the packed data-gradient weights of conv4 [32][kpad4 >= 80] and conv2
+ * [32][kpad2 >= 288] (dvie_pack_weights mode 1).  Slabs (one per workgroup, `slabs` of them):
+ * dw4 [slabs][8][288], dw2 [slabs][32][288], dw0 [slabs][32][216] (dvie_conv2d_wgrad layout,
+ * reduce with dvie_wgrad_reduce), db4 [slabs][8], db2 / db0 [slabs][32].
+ */
+typedef struct dvie_segenc_bwd_desc {
+  const void* dout;
+  const void* e2;
+  const void* e1;
+  const void* in;
+  const void* w4d;
+  const void* w2d;
+  float* dw4;
+  float* dw2;
+  float* dw0;
+  float* db4;
+  float* db2;
+  float* db0;
+  long long dout_ld, e2_ld, e1_ld, in_ld;
+  int n, h, w, kpad4;
+  int kpad2, slabs;
+} dvie_segenc_bwd_desc;
+
+int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream);
+
+/*
  * Op-list executor: runs n descriptors in order with a single host call (the per-step
  * forward and backward plans of the HRNet / VGG executors).  dvie_op.lane picks the stream:
  *   0     the caller's stream;
@@ -629,6 +659,7 @@ int dvie_segenc_fwd(const dvie_segenc_desc* d, void* stream);
 #define DVIE_OP_ATTN 12
 #define DVIE_OP_HEAD3_BWD 13
 #define DVIE_OP_SEGENC_FWD 14
+#define DVIE_OP_SEGENC_BWD 15
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
@@ -651,6 +682,7 @@ typedef struct dvie_op {
     dvie_attn_desc attn;
     dvie_head3_bwd_desc head3;
     dvie_segenc_desc segenc;
+    dvie_segenc_bwd_desc segenc_bwd;
   } u;
 } dvie_op;
 

@@ -64,11 +64,13 @@ def test_hrnet_plan_structure(dtype, fused, monkeypatch):
     # launch each (dvie_segenc_fwd)
     n_head3 = n_seg = 2 if dtype == torch.bfloat16 else 0
     assert kinds.get(L.OP_HEAD3_BWD, 0) == n_head3
-    assert kinds.get(L.OP_SEGENC_FWD, 0) == n_seg
-    assert kinds[L.OP_WGRAD] == n_ref - n_head3
+    # (forward and backward: the backward's three weight gradients and two data gradients in
+    # one dvie_segenc_bwd launch)
+    assert kinds.get(L.OP_SEGENC_FWD, 0) == n_seg and kinds.get(L.OP_SEGENC_BWD, 0) == n_seg
+    assert kinds[L.OP_WGRAD] == n_ref - n_head3 - 3 * n_seg
     n_s2 = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2)
     n_dgrad = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.x.buf.needs_grad)
-    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2 - n_head3 - 3 * n_seg
+    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2 - n_head3 - 3 * n_seg - 2 * n_seg
     # every buffer that needs a gradient received all of its contributions
     for b in g.buffers:
         if b.needs_grad and b.expected:

@@ -237,15 +237,17 @@ def test_intergan_step_matches_oracle(dev):
                                      vmasks=tr.RGBLoss.vgg_loss.vgg_net.last_plan.activation_signs(),
                                      gf_masks=fl[2], gv_masks=vl[2], df_masks=(fl[0], fl[1]), dv_masks=(vl[0], vl[1]),
                                      dtype=torch.float64)
-    bn_bias = {f"layer.{i}.bias" for i in (2, 5)}  # conv biases before BatchNorm: true gradient 0
+    # conv biases right before a train-mode BatchNorm: true gradient 0 (frame disc: layer.2;
+    # video disc: layers 2 and 5, oracle/disc.py FRAME / VIDEO)
+    bn_bias = {"f": {"layer.2.bias"}, "v": {"layer.2.bias", "layer.5.bias"}}
     moved = total = 0
     for mod, g_ref, w_ref, tag in ((m.coarse_model, g64["g"], new, "g"), (m.frame_disc_model, g64["f"], newf, "f"),
                                    (m.video_disc_model, g64["v"], newv, "v")):
         named = dict(mod.named_parameters())
         errs = {}
         for k, gr in g_ref.items():
-            if tag != "g" and k in bn_bias:
-                assert float(named[k].grad.abs().max()) < 1e-4, k
+            if k in bn_bias.get(tag, ()):  # rounding noise, relative to the layer's weight gradient
+                assert float(named[k].grad.norm()) <= 1e-3 * float(named[k[:-4] + "weight"].grad.norm()), k
                 continue
             errs[k] = rel_l2(named[k].grad, gr)
             dw = (named[k].detach().cpu().double() - w_ref[k].double()).abs()

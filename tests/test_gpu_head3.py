@@ -122,7 +122,9 @@ def test_segenc_fused_forward(dev, monkeypatch):
     nets/HRNet.py:358-364, 533-537) inside the HRNet bf16 plan at 36x100 (ragged 4 x 64
     tiles): e1 / e2 / the encoder output in the stem buffer against torch fp32 convs of the same
     bf16 operands (4e-3 relative L2: bf16 output rounding), and the whole forward + backward
-    against the unfused plan (DVIE_SEGENC_FUSED=0): outputs and gradients within 2e-2."""
+    against the unfused plan (DVIE_SEGENC_FUSED=0): outputs and gradients within 2e-2; the fused
+    backward (dvie_segenc_bwd: the encoder's weight / bias gradients with d_e2, d_e1 on chip)
+    against torch fp32 gradients from the plan's stored maps within 1e-2."""
     from deep_video_interpolation_extrapolation_amd import nets
     from deep_video_interpolation_extrapolation_amd import _lib as L
     x, seg = inputs.hrnet_input(2, 36, 100)
@@ -141,6 +143,7 @@ def test_segenc_fused_forward(dev, monkeypatch):
                 if b.t is not None and b.name.startswith(("seg0", "seg1", "feat"))}
         ((rgb * w1.to(dev)).sum() + (s * w2.to(dev)).sum()).backward()
         torch.cuda.synchronize()
+        bufs["feat_grad"] = next(b for b in plan.g.buffers if b.name == "feat").g.detach().float().cpu().clone()
         kinds = [plan.fwd_arr[i].kind for i in range(len(plan.fwd_arr))]
         res[mode] = (rgb.detach().float().cpu(), s.detach().float().cpu(), bufs,
                      {k: p.grad.detach().clone().cpu() for k, p in m.coarse_model.named_parameters()}, kinds, m)
@@ -164,3 +167,23 @@ def test_segenc_fused_forward(dev, monkeypatch):
     ga, gb = res["1"][3], res["0"][3]
     for k in gb:
         assert rel_l2(ga[k], gb[k]) < 2e-2, (k, rel_l2(ga[k], gb[k]))
+    # the fused backward (dvie_segenc_bwd) against torch fp32 on the plan's own bf16 maps:
+    # dout = the stem-buffer gradient slice, e1 / e2 / the encoder input as stored
+    assert res["1"][4].count(L.OP_SEGENC_BWD) == 0  # (forward list)
+    ref = {k: 0.0 for k in ga if k.startswith("seg_encoder")}
+    ws = [enc[i].weight.detach().cpu().to(torch.bfloat16).float() for i in (0, 2, 4)]
+    for k in range(2):
+        nchw = lambda t: t.permute(0, 3, 1, 2)  # noqa: E731
+        xin = nchw(bufs[f"seg{k}_in"])[:, :20]
+        e1, e2 = nchw(bufs[f"seg{k}_e1"]), nchw(bufs[f"seg{k}_e2"])
+        dout = nchw(bufs["feat_grad"][..., 8 * k:8 * k + 4])
+        d2 = torch.nn.grad.conv2d_input(e2.shape, ws[2], dout, padding=1) * torch.where(e2 > 0, 1.0, e2 + 1.0)
+        d1 = torch.nn.grad.conv2d_input(e1.shape, ws[1], d2, padding=1) * torch.where(e1 > 0, 1.0, e1 + 1.0)
+        for i, (gy, xx) in zip((0, 2, 4), ((d1, xin), (d2, e1), (dout, e2))):
+            ref[f"seg_encoder.{i}.weight"] = ref[f"seg_encoder.{i}.weight"] + torch.nn.grad.conv2d_weight(
+                xx, ws[i // 2].shape, gy, padding=1)
+            ref[f"seg_encoder.{i}.bias"] = ref[f"seg_encoder.{i}.bias"] + gy.sum((0, 2, 3))
+    for k, r in ref.items():
+        e = rel_l2(ga[k], r)
+        print(f"{k}: fused backward vs torch fp32 on the same maps {e:.2e}")
+        assert e < 1e-2, (k, e)  # d_e2 / d_e1 rounded to bf16 on chip
