@@ -32,8 +32,8 @@ KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwis
               8: "batchnorm_fwd", 9: "batchnorm_bwd", 10: "head_fwd", 11: "head_bwd"}
 # HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
 # this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
-PMC_DIR = "r02m_pmc"  # tools/pmc_bench.sh on the current tree
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", PMC_DIR, "traffic.json")
+# per workload; None: no PMC pass on this workload -> "traffic": null
+PMC_DIRS = {"c2": "r04census/pmc", "c5": None}
 
 
 
@@ -384,16 +384,19 @@ def main():
         by = sum(r["bytes"] for r in conv)
         tf = fl / (ms * 1e-3) / 1e12
         traffic = wg_traffic = None
-        if os.path.exists(PMC_TRAFFIC):
-            pm = json.load(open(PMC_TRAFFIC))
+        pmc_dir = PMC_DIRS.get(a.workload)
+        pmc_file = os.path.join(ROOT, "profiles", pmc_dir, "traffic.json") if pmc_dir else None
+        if pmc_file and os.path.exists(pmc_file):
+            pm = json.load(open(pmc_file))
             t, tw = pm.get("conv"), pm.get("wgrad")
             traffic = round(t["bytes_per_launch"]) if t else None
             wg_traffic = round(tw["bytes_per_launch"]) if tw else None
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                 "traffic": traffic, "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE, "
-                                                     f"profiles/{PMC_DIR})",
+                                                     f"profiles/{pmc_dir})" if traffic is not None else None,
                 "algorithmic_bytes_per_launch": round(by / max(1, n)),
-                "kernel": "conv fwd+dgrad family (conv_halo / conv_strip / conv_nk / conv1x1 / conv_igemm kernels)",
+                "kernel": "conv fwd+dgrad family (conv_h8 / conv_halo / conv_strip / conv_narrow / conv_nk / conv1x1 / "
+                          "conv_igemm / head3_bwd / segenc_fwd kernels)",
                 "launches_per_step": n // max(1, a.profile_steps),
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
                 "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4),

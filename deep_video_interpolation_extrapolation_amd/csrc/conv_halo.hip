@@ -1283,6 +1283,349 @@ static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
 }
 
 // DVIE_CONV_NK=0: narrow-input 3x3 convs on the chunked kernels (A/B runs)
+// ---------------------------------------------------------------------------------------
+// Eight-row halo tiles (conv_h8_kernel): stride-1 3x3 convs with c % 32 == 0 and
+// cout % 128 == 0 -- HRNet's 128- and 256-channel branch convs and their data gradients.
+//
+// Against conv_halo_kernel<2,2,4,3,3> (4 output rows x 64 px x 128 channels, 64-channel
+// chunks, one barrier per tap) this tile is twice as tall at half the chunk depth, so each
+// streamed weight byte feeds twice the pixels and the LDS-DMA feed per MFMA drops from
+// 24 KB to 14 KB per 16 MFMAs per wave; one tap COLUMN (3 taps, 24 KB of weights) is staged
+// per super-step, so the barrier + vmcnt wait come once per 48 MFMAs instead of 16, and the
+// weights of the next column get a whole super-step of cover.  A wave owns 64 channels x
+// 2 rows x 64 px (8 accumulators); inside a column the three taps shift the halo by one row,
+// so a B fragment row is read once per (column, slice) and used by two taps.
+//   LDS: halo 10 x 66 px x 80 B (32 channels + 16 B pad: conflict-free b128 reads for any
+//   16 consecutive pixels), double buffered (2 x 56 KB); weights 2 x 3 x (128 rows x 64 B,
+//   16-B chunks XOR-swizzled by (row >> 2) & 3) = 48 KB.  160 KB total, one workgroup per CU.
+//   Epilogue operands (residual / accumulate / activation input: EPI bits 1 / 2 / 4) are
+//   compile-time, loaded with buffer loads (out-of-range lanes read zeros, no branches).
+struct H8 {
+  static constexpr int NW = 8, NTH = 512;
+  static constexpr int BC = 128, PR = 8, KC = 32;
+  static constexpr int HR = PR + 2, HWD = 66, PITCH = 80;
+  static constexpr int HSLOTS = HR * HWD * 5;
+  static constexpr int NHI = ((HSLOTS + 63) / 64 + NW - 1) / NW * NW;
+  static constexpr int NHQ = NHI / NW;
+  static constexpr int HSZ = NHI * 1024;
+  static constexpr int ASZ = BC * KC * 2;  // one tap
+  static constexpr int WSZ = 3 * ASZ;      // one tap column
+  static constexpr int SMEM = 2 * HSZ + 2 * WSZ;
+  static constexpr int H0 = 4;             // halo pieces per wave issued in column 0 (rest in column 1)
+};
+static_assert(H8::SMEM <= 163840, "conv_h8 LDS budget");
+static_assert(H8::NHQ == 7 && H8::H0 < H8::NHQ, "halo shares");
+
+template <int EPI>
+__global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, int n_ct, int n_tiles, int tiles_x,
+                                                      int tiles_y) {
+  typedef H8 C;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave >> 2, wp = wave & 3;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nchunks = p.c >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // persistent: XCD g (= blockIdx % 8) takes a contiguous tile range, its blocks stride it
+  const int G = gridDim.x, g = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int nbg = G / 8 + (g < G % 8 ? 1 : 0);
+  const int q8 = n_tiles / 8, r8 = n_tiles % 8;
+  const int ts = g < r8 ? g * (q8 + 1) : r8 * (q8 + 1) + (g - r8) * q8;
+  const int tile0 = ts + jb, tile_end = ts + q8 + (g < r8 ? 1 : 0);
+  if (tile0 >= tile_end) return;
+
+  auto tile_job = [&](int t) {
+    JobInfo J;
+    J.t = t;
+    J.k = 0;
+    J.valid = t < tile_end;
+    J.c0 = (t % n_ct) * C::BC;
+    int pt = t / n_ct;
+    J.x0 = (pt % tiles_x) * 64;
+    pt /= tiles_x;
+    J.y0 = (pt % tiles_y) * C::PR;
+    J.n = pt / tiles_y;
+    return J;
+  };
+  auto next_job = [&](const JobInfo& J) {
+    if (J.k + 1 < nchunks) {
+      JobInfo N = J;
+      N.k = J.k + 1;
+      return N;
+    }
+    return tile_job(J.t + nbg);
+  };
+
+  // halo DMA geometry: slot -> (row, column, 16-B channel group; group 4 = pad)
+  int hgeo[C::NHQ];
+#pragma unroll
+  for (int q = 0; q < C::NHQ; ++q) {
+    const int slot = (wave + C::NW * q) * 64 + lane;
+    const int hr = slot / 5, cs = slot - 5 * (slot / 5);
+    const int hy = hr / C::HWD, hx = hr - (hr / C::HWD) * C::HWD;
+    hgeo[q] = (cs < 4 && hr < C::HR * C::HWD) ? (hy << 16) | (hx << 4) | cs : -1;
+  }
+  // weight DMA: lane fills chunk (lane & 3) of row 16*wave + (lane >> 2) from source chunk
+  // (lane & 3) ^ ((row >> 2) & 3)
+  const int arow = wave * 16 + (lane >> 2);
+  const unsigned aoff = (unsigned)arow * (unsigned)p.kpad * 2u + (unsigned)((((lane & 3) ^ ((arow >> 2) & 3))) * 16);
+  const unsigned xrow = (unsigned)p.x_ld * 2u;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const unsigned wbytes = (unsigned)p.cout * (unsigned)p.kpad * 2u;
+
+  char* const Hs = smem;
+  char* const As = smem + 2 * C::HSZ;
+
+  auto halo_issue = [&](const JobInfo& J, int hb, int qa, int qb) {
+    const int nrec = J.valid ? (int)(xbytes - (unsigned long long)J.k * 64) : 0;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)J.k * 64), 0, nrec, 0x00020000);
+    char* dst = Hs + hb * C::HSZ + wave * 1024;
+    const int ybase = J.y0 + p.dy0, xbase = J.x0 + p.dx0;
+#pragma unroll
+    for (int q = qa; q < qb; ++q) {
+      const int gq = hgeo[q];
+      const int iy = ybase + (gq >> 16), ix = xbase + ((gq >> 4) & 0xFFF);
+      const bool ok = gq >= 0 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw;
+      const unsigned o = ok ? (unsigned)((J.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)(gq & 15) * 16u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst + q * C::NW * 1024), 16, o, 0, 0, 0);
+    }
+  };
+  // tap (ti, v) of job J's tap column v into weight buffer ab (tap index ti*3 + v)
+  auto a_issue = [&](const JobInfo& J, int v, int ab, int ti) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, J.valid ? (int)wbytes : 0, 0x00020000);
+    const unsigned so = (unsigned)(J.c0 * p.kpad + (ti * 3 + v) * p.c + 32 * J.k) * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(As + ab * C::WSZ + ti * C::ASZ + wave * 1024), 16, aoff, so, 0,
+                                             0);
+  };
+
+  // fragment addresses: A row wc*64 + r32 (+32 i), chunk (2s + hh) swizzled; B pixel r32 of
+  // halo row 2*wp (+ tap row + accumulator row), channel group hh of slice s
+  const int arw = wc * 64 + r32;
+  const int a_s0 = arw * 64 + (((0 + hh) ^ ((arw >> 2) & 3)) << 4);
+  const int a_s1 = arw * 64 + (((2 + hh) ^ ((arw >> 2) & 3)) << 4);
+  const int b_base = (2 * wp * C::HWD + r32) * C::PITCH + hh * 16;
+
+  f32x16 acc[2][2][2];  // [i: 32-channel block][r: row][b: 32-pixel half]
+
+  {
+    const JobInfo J0 = tile_job(tile0);
+    halo_issue(J0, 0, 0, C::NHQ);
+#pragma unroll
+    for (int ti = 0; ti < 3; ++ti) a_issue(J0, 0, 0, ti);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  int hb = 0, ab = 0;
+  JobInfo J = tile_job(tile0);
+  JobInfo J1 = next_job(J);
+  while (J.valid) {
+    if (J.k == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][r][b][e] = 0.f;
+    }
+    const char* H = Hs + hb * C::HSZ + b_base;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const char* A = As + ab * C::WSZ;
+      const JobInfo& JW = v < 2 ? J : J1;  // owner of the next column's weights
+      const int vw = v < 2 ? v + 1 : 0;
+      i32x4 af[2][3][2], bf[2][4][2];
+      auto load_a = [&](int s, int ti) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[s][ti][i] = *(const i32x4*)(A + (s ? a_s1 : a_s0) + ti * C::ASZ + i * 2048);
+      };
+      auto load_b = [&](int s, int row) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[s][row][b] = *(const i32x4*)(H + (row * C::HWD + 32 * b + v) * C::PITCH + s * 32);
+      };
+      load_a(0, 0);
+      load_b(0, 0);
+      load_b(0, 1);
+#pragma unroll
+      for (int ph = 0; ph < 6; ++ph) {
+        const int s = ph / 3, ti = ph % 3;
+        // fragments of the next phase
+        if (ph < 5) {
+          const int s2 = (ph + 1) / 3, t2 = (ph + 1) % 3;
+          load_a(s2, t2);
+          if (t2 == 0) {
+            load_b(s2, 0);
+            load_b(s2, 1);
+          } else {
+            load_b(s2, t2 + 1);
+          }
+        }
+        // DMA: the next column's three weight taps first, then this column's halo share
+        // (the end-of-column wait counts on the halo pieces being the youngest)
+        if (ph < 3) a_issue(JW, vw, ab ^ 1, ph);
+        if (v == 0 && ph == 3) halo_issue(J1, hb ^ 1, 0, 2);
+        if (v == 0 && ph == 4) halo_issue(J1, hb ^ 1, 2, 3);
+        if (v == 0 && ph == 5) halo_issue(J1, hb ^ 1, 3, C::H0);
+        if (v == 1 && ph == 3) halo_issue(J1, hb ^ 1, C::H0, C::H0 + 1);
+        if (v == 1 && ph == 4) halo_issue(J1, hb ^ 1, C::H0 + 1, C::H0 + 2);
+        if (v == 1 && ph == 5) halo_issue(J1, hb ^ 1, C::H0 + 2, C::NHQ);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              acc[i][r][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[s][ti][i]),
+                                                                     __builtin_bit_cast(bf16x8, bf[s][ti + r][b]),
+                                                                     acc[i][r][b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // the next column's weights (and, after column 2, the next job's halo) have landed;
+      // this column's halo share may stay in flight
+      if (v == 0)
+        DVIE_VMCNT(C::H0);
+      else if (v == 1)
+        DVIE_VMCNT(C::NHQ - C::H0);
+      else
+        DVIE_VMCNT(0);
+      __builtin_amdgcn_s_barrier();
+      ab ^= 1;
+    }
+    hb ^= 1;
+
+    if (J.k + 1 == nchunks) {
+      // ---- epilogue: eight groups (channel block i, row r, pixel half b), one accumulator each; the
+      // operands of group g+1 are issued before the arithmetic of group g ----
+      const long long pix0 = ((long long)J.n * p.yh + (long long)J.y0 * p.osy + p.ory) * p.yw + (long long)J.x0 * p.osx + p.orx;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const bf16_t*)p.res + ((EPI & 1) ? pix0 * p.res_ld : 0)), 0, 0x7FFFFFF0, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rb =
+          __builtin_amdgcn_make_buffer_rsrc((void*)((const bf16_t*)p.y + pix0 * p.y_ld), 0, 0x7FFFFFF0, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const bf16_t*)p.z + ((EPI & 4) ? pix0 * p.z_ld : 0)), 0, 0x7FFFFFF0, 0x00020000);
+      i32x4 o_r[2][2], o_b[2][2], o_z[2][2];  // [buffer][P]
+      auto epi_load = [&](int gi) {
+        const int i = gi >> 2, r = (gi >> 1) & 1, b = gi & 1, u = gi & 1;
+#pragma unroll
+          for (int P = 0; P < 2; ++P) {
+            const int oy = J.y0 + 2 * wp + r, ox = J.x0 + 32 * b + r32;
+            const int co = J.c0 + wc * 64 + 32 * i + 16 * P + 8 * hh;
+            const bool ok = oy < p.oh && ox < p.ow;
+            const long long dp = (long long)(2 * wp + r) * p.osy * p.yw + (long long)(32 * b + r32) * p.osx;
+            if (EPI & 1) o_r[u][P] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? (unsigned)((dp * p.res_ld + co) * 2) : OOB, 0, 0);
+            if (EPI & 2) o_b[u][P] = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? (unsigned)((dp * p.y_ld + co) * 2) : OOB, 0, 0);
+            if (EPI & 4) o_z[u][P] = __builtin_amdgcn_raw_buffer_load_b128(rz, ok ? (unsigned)((dp * p.z_ld + co) * 2) : OOB, 0, 0);
+          }
+      };
+      if (EPI) epi_load(0);
+#pragma unroll
+      for (int gi = 0; gi < 8; ++gi) {
+        const int i = gi >> 2, r = (gi >> 1) & 1, b = gi & 1, u = gi & 1;
+        if (EPI && gi < 7) epi_load(gi + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        {
+          float v8[2][8];
+#pragma unroll
+          for (int P = 0; P < 2; ++P)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][r][b][8 * P + e]),
+                                                               __float_as_uint(acc[i][r][b][8 * P + 4 + e]), false, false);
+              v8[P][e] = __uint_as_float(sw[0]);
+              v8[P][4 + e] = __uint_as_float(sw[1]);
+            }
+          const int oy = J.y0 + 2 * wp + r, ox = J.x0 + 32 * b + r32;
+          const bool ok = oy < p.oh && ox < p.ow;
+          const long long dp = (long long)(2 * wp + r) * p.osy * p.yw + (long long)(32 * b + r32) * p.osx;
+#pragma unroll
+          for (int P = 0; P < 2; ++P) {
+            const int co = J.c0 + wc * 64 + 32 * i + 16 * P + 8 * hh;
+            float* w = v8[P];
+            if (p.bias) {
+              const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[e] += b0[e];
+                w[4 + e] += b1[e];
+              }
+            }
+            if (EPI & 1) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[2 * e] += __uint_as_float(((uint32_t)o_r[u][P][e]) << 16);
+                w[2 * e + 1] += __uint_as_float(((uint32_t)o_r[u][P][e]) & 0xffff0000u);
+              }
+            }
+            if (EPI & 2) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[2 * e] += __uint_as_float(((uint32_t)o_b[u][P][e]) << 16);
+                w[2 * e + 1] += __uint_as_float(((uint32_t)o_b[u][P][e]) & 0xffff0000u);
+              }
+            }
+            act_apply(w, 8, p.act, p.alpha);
+            if (EPI & 4) {
+              float z[8];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                z[2 * e] = __uint_as_float(((uint32_t)o_z[u][P][e]) << 16);
+                z[2 * e + 1] = __uint_as_float(((uint32_t)o_z[u][P][e]) & 0xffff0000u);
+              }
+              dact_apply(w, z, 8, p.dact, p.alpha);
+            }
+            i32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
+            if (ok) __builtin_amdgcn_raw_buffer_store_b128(o, rb, (unsigned)((dp * p.y_ld + co) * 2), 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    J = J1;
+    J1 = next_job(J1);
+  }
+}
+
+// DVIE_CONV_H8=0: the 4-row halo kernel takes these convs (A/B runs); read per launch
+static bool h8_on() {
+  const char* e = getenv("DVIE_CONV_H8");
+  return !(e && *e == '0');
+}
+
+template <int EPI>
+static void launch_h8(const dvie_conv_desc& p, hipStream_t s, int n_ct, int n_tiles, int tiles_x, int tiles_y) {
+  const int grid = n_tiles > 256 ? 256 : n_tiles;
+  hipLaunchKernelGGL((conv_h8_kernel<EPI>), dim3(grid), dim3(H8::NTH), 0, s, p, n_ct, n_tiles, tiles_x, tiles_y);
+}
+
+// 3x3 stride-1 conv, identity taps (t3), bf16 output; true when the eight-row kernel took it
+static bool conv_h8_launch(const dvie_conv_desc& p, hipStream_t s) {
+  if (!h8_on() || p.out_f32 || p.c % 32 != 0 || p.c < 64 || p.cout % 128 != 0) return false;
+  const int n_ct = p.cout / H8::BC, tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + H8::PR - 1) / H8::PR;
+  const long long nt = (long long)n_ct * tiles_x * tiles_y * p.n;
+  if (nt < 224 || nt >= (1LL << 30)) return false;  // fewer tiles than CUs: the 4-row kernel
+  const int n_tiles = (int)nt;
+  switch ((p.res ? 1 : 0) | (p.beta ? 2 : 0) | (p.dact ? 4 : 0)) {
+    case 0: launch_h8<0>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    case 1: launch_h8<1>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    case 2: launch_h8<2>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    case 3: launch_h8<3>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    case 4: launch_h8<4>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    case 5: launch_h8<5>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    case 6: launch_h8<6>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+    default: launch_h8<7>(p, s, n_ct, n_tiles, tiles_x, tiles_y); break;
+  }
+  return true;
+}
+
 static const bool nk_env_off = getenv("DVIE_CONV_NK") && *getenv("DVIE_CONV_NK") == '0';
 
 bool conv_narrow_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_narrow.hip
@@ -1324,6 +1667,7 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
   // <= 32 output channels from > 64 input channels (the HRNet heads): one step per 32-channel
   // chunk with all 9 taps (conv_narrow.hip)
   if (t3 && cfg == -3 && conv_narrow_launch(p, s)) return true;
+  if (t3 && cfg == -3 && conv_h8_launch(p, s)) return true;
   if (cfg < 0) {  // measured on MI355X (tools/conv_tune.py): see DESIGN.md
     if (p.cout <= 32)
       cfg = 2;

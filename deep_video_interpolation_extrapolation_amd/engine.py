@@ -790,7 +790,10 @@ class Plan:
         g = self.g
         nf = self.nf
         fused_first, skip = {}, set()
-        for chain in getattr(g, "segenc", []):
+        # the fused forward measured slower than its three convs at 8x256x512 (0.555 vs 0.40 ms
+        # per step, profiles/r04e/ops.txt): opt-in (DVIE_SEGENC_FWD=1); the fused backward stays
+        fwd_on = os.environ.get("DVIE_SEGENC_FWD", "0") == "1"
+        for chain in getattr(g, "segenc", []) if fwd_on else []:
             if self._segenc_fusable(chain):
                 fused_first[id(chain[0])] = chain
                 skip.update(id(op) for op in chain[1:])
@@ -1323,9 +1326,14 @@ class Plan:
 
     def _head3_fusable(self, op, gld):
         """Narrow-output 3x3 head conv (HRNet rgb_layer[2] / seg_layer[2]) whose backward can
-        run as one dvie_head3_bwd pass over its input (DVIE_HEAD3_FUSED=0: unfused)."""
+        run as one dvie_head3_bwd pass over its input.  DVIE_HEAD3_FUSED: 1 (default) the rgb
+        head (8 padded channels) only -- measured 0.905 -> 0.655 ms per step, while the fused
+        seg head (24) ran 1.274 ms against 1.059 unfused (profiles/r04e/ops.txt); 2 both; 0 none."""
         lay, x, out = op.layer, op.x, op.out
-        if self.dtype != torch.bfloat16 or os.environ.get("DVIE_HEAD3_FUSED", "1") == "0":
+        mode = os.environ.get("DVIE_HEAD3_FUSED", "1")
+        if self.dtype != torch.bfloat16 or mode == "0" or (mode == "1" and lay.cout_p != 8):
+            return False
+        if os.environ.get("DVIE_IM2COL_DGRAD", "0") == "1":  # the opt-in im2col lowering asked for
             return False
         if not (lay.trainable and x.buf.needs_grad and op.res is None and lay.kh == 3 and lay.kw == 3
                 and lay.stride == 1 and lay.pad == 1 and lay.dil == 1 and lay.cout_p in (8, 24)

@@ -296,10 +296,13 @@ class _PlanDiscriminator(FlatParams, nn.Module):
     def run_backward(self, plan, inputs, grads, needs):
         (go,) = grads
         dev = inputs[0].device
-        trainable = any(p.requires_grad for p in self.parameters())
+        pn = getattr(self, "_param_needs", None)
+        sel = None if pn is None else [p for p, nd in zip(self._flat_params, pn) if nd]
+        trainable = any(p.requires_grad for p in self.parameters()) if sel is None else bool(sel)
         accumulate = False
         if trainable:
-            accumulate = self.grad_views()
+            # (SpectralNorm u / v: a gradient only when they required one at the forward)
+            accumulate = self.grad_views(sel)
             # SN convs: this call's d(W_bar / sigma) overwrites module.weight.grad (scratch)
             plan.set_param_grads(accumulate, fresh={id(s.module) for s in self._sn})
         if self.local:

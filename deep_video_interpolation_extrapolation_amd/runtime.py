@@ -173,6 +173,9 @@ class PlanFunction(torch.autograd.Function):
         if plan.generation != ctx.gen:
             raise RuntimeError("plan activations were overwritten before backward")
         inputs = ctx.saved_tensors
+        # parameters get a gradient only if they required one at the forward (autograd's rule:
+        # a later requires_grad_(True) does not reach back into this graph)
+        ctx.runner._param_needs = tuple(ctx.needs_input_grad[2 + ctx.n_in:])
         in_grads = ctx.runner.run_backward(plan, inputs, grads, ctx.needs_input_grad[2:2 + ctx.n_in])
         plan.busy = False
         ctx.token = None

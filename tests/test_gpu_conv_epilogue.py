@@ -147,3 +147,23 @@ def test_conv_strip_fp32_out(dev, mode, strip, monkeypatch):
     monkeypatch.setenv("DVIE_CONV_STRIP", strip)
     err = _run(dev, (2, 131, 250, 64, 64, 3), mode, out_f32=True)
     assert err < 1e-2, (mode, strip, err)
+
+
+H8_SHAPES = [  # 3x3, c % 32 == 0, cout % 128 == 0, >= 224 eight-row tiles: conv_h8_kernel
+    (4, 125, 250, 128, 128, 3),   # ragged rows and columns, one tile per workgroup
+    (8, 61, 120, 256, 256, 3),    # two 128-channel tiles per pixel tile, 8 chunks
+    (5, 128, 160, 96, 128, 3),    # 3 chunks of 32 channels
+    (3, 200, 256, 128, 128, 3),   # 300 tiles: workgroups run one or two tiles
+]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", H8_SHAPES)
+def test_conv_h8_modes(dev, shape, mode, monkeypatch):
+    """The eight-row halo kernel and, for comparison, the four-row halo kernel it replaces on
+    these shapes (DVIE_CONV_H8=0): every epilogue operand set."""
+    errs = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("DVIE_CONV_H8", env)
+        errs[env] = _run(dev, shape, mode)
+    assert errs["1"] < 1e-2 and errs["0"] < 1e-2, (shape, mode, errs)
