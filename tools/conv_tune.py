@@ -1,7 +1,7 @@
 """Time dvie_conv2d_fwd per tile configuration on HRNet-shaped convolutions and check each
 result against torch's fp32 conv2d of the same bf16-rounded operands.
 
-    python tools/conv_tune.py [cfgs] [iters] [shape-substring]   e.g.  python tools/conv_tune.py -1,0,1 20 '64->64'
+    python tools/conv_tune.py [cfgs] [iters] [shape-substring]   e.g.  python tools/conv_tune.py -1,0,1 20 '64->64'   (several: '128->128|256->256')
 """
 import ctypes
 import os
@@ -42,7 +42,7 @@ def main():
     s = L.stream_ptr()
     first = True
     for name, cin, cout, k, H, W, B in SHAPES:
-        if only and only not in name:
+        if only and not any(o in name for o in only.split("|")):
             continue
         torch.manual_seed(0)
         out_f32 = "f32out" in name
