@@ -11,8 +11,6 @@
 
 namespace dvie {
 
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-
 // torch.linspace(-1, 1, n)[i] as computed by the CPU kernel (two-sided)
 __device__ __forceinline__ float linspace_pm1(int i, int n) {
   if (n <= 1) return -1.f;
@@ -166,117 +164,6 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
           warp_corners(im, t[k], p.w, a, b, cc, d, pair[k]);
           o[k] = warp_blend(a, b, cc, d, t[k]);
         }
-        store(c, o);
-      }
-    }
-  }
-}
-
-// Forward, two adjacent pixels per lane (CC = 3, even widths): a wave covers 512 consecutive
-// pixels of a row, lane owning the pairs (x, x + 1) at x = 2 lane + 128 k, k < 4.  Flow loads
-// and output stores are 8-byte pairs.  When (wave-uniform) every pair's two samples share
-// their corner rows and their corner columns fit in x0 .. x0 + 3 of the first one (a smooth
-// flow: neighbouring samples move together), ONE 16-byte load per corner row serves both
-// pixels of a pair: 2 gathers per channel for 2 pixels instead of 4, and half the flow-load
-// and store instructions.  Otherwise the pairs take the one-pixel corner loads.  The blend is
-// warp_blend's, so the outputs equal warp_fwd_kernel's bit for bit.
-template <int CC>
-__global__ __launch_bounds__(256) void warp_fwd2_kernel(const dvie_warp_desc p) {
-  const int segs = (p.w + 511) >> 9;
-  const long long hw = (long long)p.h * p.w;
-  const int waves = p.n * p.h * segs;
-  const int lane = threadIdx.x & 63;
-  constexpr unsigned kOut = 0x80000000u;
-  for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
-       wv += gridDim.x * 4) {
-    const int sg = wv % segs;
-    const int r = wv / segs;
-    const int y = r % p.h, n = r / p.h;
-    const __amdgpu_buffer_rsrc_t rf0 = warp_plane(p.flow + (long long)n * 2 * hw, hw);
-    const __amdgpu_buffer_rsrc_t rf1 = warp_plane(p.flow + ((long long)n * 2 + 1) * hw, hw);
-    float fx[4][2], fy[4][2];
-    bool live[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int x = (sg << 9) + 2 * lane + 128 * k;
-      live[k] = x < p.w;  // (even width: the pair is live or dead as a whole)
-      const unsigned fo = (unsigned)(y * p.w + (live[k] ? x : p.w - 2)) * 4u;
-      const auto a = __builtin_amdgcn_raw_buffer_load_b64(rf0, fo, 0, 0);
-      const auto b = __builtin_amdgcn_raw_buffer_load_b64(rf1, fo, 0, 0);
-      fx[k][0] = __uint_as_float(a[0]);
-      fx[k][1] = __uint_as_float(a[1]);
-      fy[k][0] = __uint_as_float(b[0]);
-      fy[k][1] = __uint_as_float(b[1]);
-    }
-    WarpTap t[4][2];
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int x = live[k] ? (sg << 9) + 2 * lane + 128 * k : p.w - 2;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) t[k][e] = warp_tap(x + e, y, fx[k][e], fy[k][e], p.w, p.h, p.align_corners);
-      const int dx = t[k][1].x0 - t[k][0].x0;
-      ok = ok && t[k][1].y0 == t[k][0].y0 && dx >= 0 && dx <= 2 && t[k][0].x0 >= 0 && t[k][0].x0 + 3 < p.w;
-    }
-    const bool fast = __all(ok);
-    auto store = [&](int c, const float (*o)[2]) {
-      const __amdgpu_buffer_rsrc_t out = warp_plane(p.out + ((long long)n * CC + c) * hw, hw);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {  // dead pairs: out-of-range offset, store dropped
-        const unsigned off = live[k] ? (unsigned)(y * p.w + (sg << 9) + 2 * lane + 128 * k) * 4u : kOut;
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, (f32x2_t{o[k][0], o[k][1]})), out, off, 0, 0);
-      }
-    };
-    if (fast) {
-      i32x4 u[CC][4], v[CC][4];
-#pragma unroll
-      for (int c = 0; c < CC; ++c) {
-        const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + ((long long)n * CC + c) * hw, hw);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const WarpTap& t0 = t[k][0];
-          const unsigned r0 = (unsigned)(t0.y0 * p.w + t0.x0), r1 = (unsigned)((t0.y0 + 1) * p.w + t0.x0);
-          u[c][k] = __builtin_amdgcn_raw_buffer_load_b128(im, t0.vy0 ? r0 * 4u : kOut, 0, 0);
-          v[c][k] = __builtin_amdgcn_raw_buffer_load_b128(im, t0.vy1 ? r1 * 4u : kOut, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < CC; ++c) {
-        float o[4][2];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int dx = t[k][1].x0 - t[k][0].x0;
-          const i32x4 uu = u[c][k], vv = v[c][k];
-          o[k][0] = warp_blend(__int_as_float(uu[0]), __int_as_float(uu[1]), __int_as_float(vv[0]),
-                               __int_as_float(vv[1]), t[k][0]);
-          const int ua = dx == 0 ? uu[0] : dx == 1 ? uu[1] : uu[2];
-          const int ub = dx == 0 ? uu[1] : dx == 1 ? uu[2] : uu[3];
-          const int va = dx == 0 ? vv[0] : dx == 1 ? vv[1] : vv[2];
-          const int vb = dx == 0 ? vv[1] : dx == 1 ? vv[2] : vv[3];
-          o[k][1] = warp_blend(__int_as_float(ua), __int_as_float(ub), __int_as_float(va), __int_as_float(vb), t[k][1]);
-        }
-        store(c, o);
-      }
-    } else {
-      float vv[CC][4][2][4];
-#pragma unroll
-      for (int c = 0; c < CC; ++c) {
-        const __amdgpu_buffer_rsrc_t im = warp_plane(p.img + ((long long)n * CC + c) * hw, hw);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int e = 0; e < 2; ++e)
-            warp_corners(im, t[k][e], p.w, vv[c][k][e][0], vv[c][k][e][1], vv[c][k][e][2], vv[c][k][e][3]);
-      }
-#pragma unroll
-      for (int c = 0; c < CC; ++c) {
-        float o[4][2];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int e = 0; e < 2; ++e)
-            o[k][e] = warp_blend(vv[c][k][e][0], vv[c][k][e][1], vv[c][k][e][2], vv[c][k][e][3], t[k][e]);
         store(c, o);
       }
     }
@@ -627,8 +514,6 @@ __global__ void scale_kernel(float* p, long long n, float s) {
     p[i] *= s;
 }
 
-// DVIE_WARP_FWD2=0: the one-pixel-per-lane forward (A/B runs); read once
-static const bool warp_fwd2_on = !(getenv("DVIE_WARP_FWD2") && *getenv("DVIE_WARP_FWD2") == '0');
 
 static int grid_for(long long n) {
   long long b = (n + 255) / 256;
@@ -648,10 +533,7 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
   DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
   const int grid = grid_for(waves * 256);
-  if (d->c == 3 && d->w % 2 == 0 && d->w >= 4 && warp_fwd2_on) {
-    const long long waves2 = (long long)d->n * d->h * ((d->w + 511) / 512);
-    hipLaunchKernelGGL(warp_fwd2_kernel<3>, dim3(grid_for(waves2 * 256)), dim3(256), 0, (hipStream_t)stream, *d);
-  } else if (d->c == 3)
+  if (d->c == 3)
     hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
   else
     hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
