@@ -104,6 +104,8 @@ struct HaloCfg {
 
 // s_waitcnt vmcnt(n) only (expcnt / lgkmcnt left at their maxima)
 #define DVIE_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
+// vmcnt(n) and lgkmcnt(0) together
+#define DVIE_VMCNT_LGKM0(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4))
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
 #define DVIE_VMCASE(N) \
@@ -1294,7 +1296,10 @@ static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
 // per super-step, so the barrier + vmcnt wait come once per 48 MFMAs instead of 16, and the
 // weights of the next column get a whole super-step of cover.  A wave owns 64 channels x
 // 2 rows x 64 px (8 accumulators); inside a column the three taps shift the halo by one row,
-// so a B fragment row is read once per (column, slice) and used by two taps.
+// so a B fragment row is read once per (column, slice) and used by two taps.  The column's
+// wait + barrier sit before its last eight MFMAs, which then cover the LDS round trip of the
+// next column's first fragments (same box: 256 -> 256 66.9 -> 65.2 us, step 221.2 -> 223.6
+// frames/s, profiles/r04h8b/).
 //   LDS: halo 10 x 66 px x 80 B (32 channels + 16 B pad: conflict-free b128 reads for any
 //   16 consecutive pixels), double buffered (2 x 56 KB); weights 2 x 3 x (128 rows x 64 B,
 //   16-B chunks XOR-swizzled by (row >> 2) & 3) = 48 KB.  160 KB total, one workgroup per CU.
@@ -1423,6 +1428,19 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
   int hb = 0, ab = 0;
   JobInfo J = tile_job(tile0);
   JobInfo J1 = next_job(J);
+  // phase-0 fragments of a column (A: tap row 0, slice 0; B: halo rows 0 and 1, slice 0).
+  // They are loaded right after the barrier that ends the previous column, under that
+  // column's last eight MFMAs, so no column starts on an LDS round trip.
+  i32x4 pa[2], pb[2][2];
+  auto load_p0 = [&](const char* A0, const char* H0, int v0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) pa[i] = *(const i32x4*)(A0 + a_s0 + i * 2048);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) pb[r][b] = *(const i32x4*)(H0 + (r * C::HWD + 32 * b + v0) * C::PITCH);
+  };
+  load_p0(As, Hs + b_base, 0);
   while (J.valid) {
     if (J.k == 0) {
 #pragma unroll
@@ -1435,6 +1453,7 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
             for (int e = 0; e < 16; ++e) acc[i][r][b][e] = 0.f;
     }
     const char* H = Hs + hb * C::HSZ + b_base;
+    const bool tile_end_job = J.k + 1 == nchunks;  // the epilogue follows this job
 #pragma unroll
     for (int v = 0; v < 3; ++v) {
       const char* A = As + ab * C::WSZ;
@@ -1449,9 +1468,12 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
 #pragma unroll
         for (int b = 0; b < 2; ++b) bf[s][row][b] = *(const i32x4*)(H + (row * C::HWD + 32 * b + v) * C::PITCH + s * 32);
       };
-      load_a(0, 0);
-      load_b(0, 0);
-      load_b(0, 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[0][0][i] = pa[i];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[0][r][b] = pb[r][b];
 #pragma unroll
       for (int ph = 0; ph < 6; ++ph) {
         const int s = ph / 3, ti = ph % 3;
@@ -1475,6 +1497,23 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
         if (v == 1 && ph == 3) halo_issue(J1, hb ^ 1, C::H0, C::H0 + 1);
         if (v == 1 && ph == 4) halo_issue(J1, hb ^ 1, C::H0 + 1, C::H0 + 2);
         if (v == 1 && ph == 5) halo_issue(J1, hb ^ 1, C::H0 + 2, C::NHQ);
+        if (ph == 5) {
+          // end of the column before its last MFMAs: the next column's weights (and, after
+          // column 2, the next job's halo) have landed -- this column's halo share may stay
+          // in flight -- and every wave's reads of this column's weight buffer are done
+          // (lgkmcnt 0), so the buffer may be refilled after the barrier
+          if (v == 0)
+            DVIE_VMCNT_LGKM0(C::H0);
+          else if (v == 1)
+            DVIE_VMCNT_LGKM0(C::NHQ - C::H0);
+          else
+            DVIE_VMCNT_LGKM0(0);
+          __builtin_amdgcn_s_barrier();
+          if (v < 2)
+            load_p0(As + (ab ^ 1) * C::WSZ, H, v + 1);
+          else if (!tile_end_job)
+            load_p0(As + (ab ^ 1) * C::WSZ, Hs + (hb ^ 1) * C::HSZ + b_base, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -1487,15 +1526,6 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
                                                                      acc[i][r][b], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      // the next column's weights (and, after column 2, the next job's halo) have landed;
-      // this column's halo share may stay in flight
-      if (v == 0)
-        DVIE_VMCNT(C::H0);
-      else if (v == 1)
-        DVIE_VMCNT(C::NHQ - C::H0);
-      else
-        DVIE_VMCNT(0);
-      __builtin_amdgcn_s_barrier();
       ab ^= 1;
     }
     hb ^= 1;
@@ -1588,6 +1618,7 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      load_p0(As + ab * C::WSZ, Hs + hb * C::HSZ + b_base, 0);  // the next job's first column
     }
     J = J1;
     J1 = next_job(J1);
