@@ -7,6 +7,8 @@ tag=${1:-census}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/$tag
 mkdir -p $out
+timeout -k 10 420 python -u bench.py --ops-out $out/ops.txt > $out/bench.json 2> $out/bench.err || { echo "bench failed"; tail -20 $out/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('$out/bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['frac'])"
 for k in 2 6; do
   DVIE_OP_LANES=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/s$k -o run \
     -- python3 bench.py --steps $k --warmup 1 --no-cpu-baseline --profile-steps 0 > $out/s$k.log 2>&1 \
