@@ -16,4 +16,8 @@ timeout -k 10 420 python -u bench.py > $out/bench.json 2> $out/bench.err || { ec
 cat $out/bench.json
 DVIE_OP_LANES=0 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o bench -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-steps 0 --graph 0 > $out/bench_prof.json 2> $out/bench_prof.err || { echo "rocprof failed"; tail -20 $out/bench_prof.err; exit 1; }
 find $out/prof -name '*kernel_stats.csv' -exec head -12 {} \;
+if [ "$3" == "c5" ]; then  # BASELINE config 5 line with its per-op table
+  timeout -k 10 600 python -u bench.py --workload c5 --ops-out $out/ops_c5.txt > $out/bench_c5.json 2> $out/bench_c5.err || { echo "c5 bench failed"; tail -20 $out/bench_c5.err; exit 1; }
+  cat $out/bench_c5.json
+fi
 echo done
