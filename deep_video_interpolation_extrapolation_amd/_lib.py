@@ -79,7 +79,7 @@ class PackDesc(ctypes.Structure):
         ("rows", i32), ("kpad", i32), ("c", i32), ("mode", i32),
         ("th", i32), ("tw", i32), ("kh0", i32), ("kw0", i32),
         ("dkh", i32), ("dkw", i32), ("cout_s", i32), ("cin_s", i32),
-        ("kh_s", i32), ("kw_s", i32), ("dtype", i32), ("pad0", i32),
+        ("kh_s", i32), ("kw_s", i32), ("dtype", i32), ("blk0", i32),
     ]
 
 
@@ -175,7 +175,7 @@ class AttnDesc(ctypes.Structure):
 
 
 class PackList(ctypes.Structure):
-    _fields_ = [("descs_dev", vp), ("n", i32), ("max_elems", i32)]
+    _fields_ = [("descs_dev", vp), ("n", i32), ("blocks", i32)]
 
 
 class Head3BwdDesc(ctypes.Structure):

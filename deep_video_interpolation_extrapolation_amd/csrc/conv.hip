@@ -344,17 +344,35 @@ __global__ __launch_bounds__(256) void colsum_kernel(const dvie_colsum_desc p, l
   }
 }
 
-__global__ void pack_kernel(const dvie_pack_desc* __restrict__ descs) {
-  const dvie_pack_desc p = descs[blockIdx.y];
+// Flat grid: block b belongs to the last descriptor whose blk0 <= b (uniform binary search);
+// a thread packs 4 consecutive elements of its descriptor (one 8-byte bf16 store when the
+// four share a row).  The earlier (block x, descriptor y) grid launched max-size x blocks for
+// every descriptor, nearly all of them empty: 0.29 ms per step for ~40 MB of weights.
+__global__ __launch_bounds__(256) void pack_kernel(const dvie_pack_desc* __restrict__ descs, int n) {
+  int lo = 0, hi = n - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].blk0 <= b)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  const dvie_pack_desc p = descs[lo];
   const long long total = (long long)p.rows * p.kpad;
+  const long long e0 = ((long long)(b - p.blk0) * 256 + threadIdx.x) * 4;
+  if (e0 >= total) return;
   const int ntap = p.th * p.tw;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
+  float v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long long e = e0 + q;
+    v[q] = 0.f;
+    if (e >= total) continue;
     const int r = (int)(e / p.kpad);
     const int k = (int)(e - (long long)r * p.kpad);
     const int t = k / p.c;
     const int j = k - t * p.c;
-    float v = 0.f;
     if (t < ntap) {
       int co, ci;
       if (p.mode == 0) {
@@ -367,12 +385,24 @@ __global__ void pack_kernel(const dvie_pack_desc* __restrict__ descs) {
       const int kh = p.kh0 + (t / p.tw) * p.dkh;
       const int kw = p.kw0 + (t % p.tw) * p.dkw;
       if (co < p.cout_s && ci >= 0 && ci < p.cin_s && kh >= 0 && kh < p.kh_s && kw >= 0 && kw < p.kw_s)
-        v = p.src[(((long long)co * p.cin_s + ci) * p.kh_s + kh) * p.kw_s + kw];
+        v[q] = p.src[(((long long)co * p.cin_s + ci) * p.kh_s + kh) * p.kw_s + kw];
     }
-    if (p.dtype == DVIE_BF16)
-      ((bf16_t*)p.dst)[e] = f2bf(v);
-    else
-      ((float*)p.dst)[e] = v;
+  }
+  if (p.dtype == DVIE_BF16) {
+    bf16_t* d = (bf16_t*)p.dst + e0;
+    if (e0 + 4 <= total && p.kpad % 4 == 0) {  // four of one row, 8-byte aligned
+      uint2 u;
+      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *(uint2*)d = u;
+    } else {
+      for (int q = 0; q < 4; ++q)
+        if (e0 + q < total) d[q] = f2bf(v[q]);
+    }
+  } else {
+    float* d = (float*)p.dst + e0;
+    for (int q = 0; q < 4; ++q)
+      if (e0 + q < total) d[q] = v[q];
   }
 }
 
@@ -473,12 +503,9 @@ int dvie_colsum(const dvie_colsum_desc* d, void* stream) {
   DVIE_RETURN_LAUNCH();
 }
 
-int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, void* stream) {
-  DVIE_CHECK_ARG(descs_dev && n > 0 && n < 65536, "pack: args");
-  int blocks = (max_elems + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(pack_kernel, dim3(blocks, n), dim3(256), 0, (hipStream_t)stream, descs_dev);
+int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int blocks, void* stream) {
+  DVIE_CHECK_ARG(descs_dev && n > 0 && blocks > 0, "pack: args (n %d, blocks %d)", n, blocks);
+  hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, descs_dev, n);
   DVIE_RETURN_LAUNCH();
 }
 

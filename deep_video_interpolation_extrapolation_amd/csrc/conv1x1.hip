@@ -92,7 +92,10 @@ struct G1Cfg {
 // PRE (bf16 output, single K-step only): epilogue operands loaded into registers right after
 // the stage's DMA, so their HBM latency overlaps the operand DMA instead of following the
 // MFMAs (1 residual, 2 accumulate target, 4 activation input).
-template <int TMC, int NS, int KC, int NWP, int MI, int NWC, bool OUTF32, int PRE = 0>
+// CE (bf16 output, MI = 1, 8 accumulator chunks per lane, identity placement, full channel
+// tiles): the packed outputs are transposed across each 8-lane group (three xor-shuffle
+// stages), so store instruction k writes 4 whole pixels x 256 B instead of 32 pixels x 32 B.
+template <int TMC, int NS, int KC, int NWP, int MI, int NWC, bool OUTF32, int PRE = 0, bool CE = false>
 __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv_desc p, int n_ct, int n_tiles, int dbg) {
   dbg = DVIE_DBG(dbg);
   typedef G1Cfg<TMC, NS, KC, NWP, MI, NWC> C;
@@ -257,9 +260,12 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
 
   // ---- epilogue: lane owns pixel wp*32*MI + 32*i + r32; after permlane32 pairing, lane half h
   // holds channels 16P + 8h .. +7 of pair P of each 32-channel accumulator
+  static_assert(!CE || (MI == 1 && 2 * TMC == 8 && !OUTF32), "coalesced epilogue: 8 chunks per lane");
+  i32x4 ob[CE ? 8 : 1];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-  const int pix = p0 + wp * 32 * MI + 32 * i + r32;
+  const int pix0 = p0 + wp * 32 * MI + 32 * i + r32;
+  const int pix = CE ? min(pix0, npix - 1) : pix0;  // (CE: every lane takes part in the shuffles)
   float v[TMC][2][8];
 #pragma unroll
   for (int j = 0; j < TMC; ++j)
@@ -272,7 +278,7 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
         v[j][P][e] = __uint_as_float(sw[0]);
         v[j][P][4 + e] = __uint_as_float(sw[1]);
       }
-  if (pix >= npix) continue;
+  if (!CE && pix >= npix) continue;
   long long yp = pix;
   if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) {
     const int hw = p.oh * p.ow;
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
       const int co = c0 + wc * 32 * TMC + 32 * j + 16 * P + 8 * hh;
-      if (co >= p.cout) continue;
+      if (!CE && co >= p.cout) continue;
       float* w = v[j][P];
       if (p.bias) {
         const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
@@ -352,8 +358,40 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
         i32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = (int)pk_bf16(w[2 * e], w[2 * e + 1]);
-        if (!(dbg & 1) || w[0] == 12345.678f) *(i32x4*)dst = o;
+        if constexpr (CE)
+          ob[2 * j + P] = o;
+        else if (!(dbg & 1) || w[0] == 12345.678f)
+          *(i32x4*)dst = o;
       }
+    }
+  }
+  if constexpr (CE) {
+    // 8 x 8 transpose of 16-B chunks inside each 8-lane group (lane b, chunk k) -> (k, b):
+    // at distance d the lane with bit d set trades its chunk k for the partner's chunk k + d
+    const int b = lane & 7;
+#pragma unroll
+    for (int d = 4; d >= 1; d >>= 1) {
+      const bool up = (b & d) != 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (k & d) continue;
+        const i32x4 t = up ? ob[k] : ob[k + d];
+        i32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = __shfl_xor(t[e], d);
+        if (up)
+          ob[k] = r;
+        else
+          ob[k + d] = r;
+      }
+    }
+    // lane (h, 8a + b) now holds pixel 8a + k, channels 32 (b / 2) + 16 (b % 2) + 8 h of chunk k
+    const int a8 = r32 >> 3;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int px = p0 + wp * 32 + 8 * a8 + k;
+      const int co = c0 + wc * 32 * TMC + 32 * (b >> 1) + 16 * (b & 1) + 8 * hh;
+      if (px < npix) *(i32x4*)((bf16_t*)p.y + (long long)px * p.y_ld + co) = ob[k];
     }
   }
 }
@@ -577,6 +615,13 @@ static int dbg_env() {
 #endif
 }
 
+// DVIE_1X1_CE=0: the MFMA-layout epilogue stores for the single-K-step wide tiles (A/B runs);
+// read per launch
+static bool ce_env_on() {
+  const char* e = getenv("DVIE_1X1_CE");
+  return !(e && *e == '0');
+}
+
 // DVIE_1X1_PRE=0: no epilogue-operand prefetch (A/B runs); read per launch
 static bool pre_env_on() {
   const char* e = getenv("DVIE_1X1_PRE");
@@ -613,6 +658,20 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   if constexpr (NS == 1) {
     if (ident && p.c <= KC && pre_env_on()) {
       pre = MI * TMC > 4 ? 0 : (p.res ? 1 : 0) | (p.beta ? 2 : 0) | (p.dact ? 4 : 0);
+    }
+  }
+  if constexpr (NS == 1 && MI == 1 && 2 * TMC == 8) {
+    if (ident && ce_env_on() && p.cout % C::BC == 0) {
+      switch (pre) {
+#define DVIE_1X1_CE_CASE(V)                                                                                          \
+  case V:                                                                                                            \
+    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false, PreOk<V, NS, MI * TMC>::v, true>), dim3(n_tiles), \
+                       dim3(64 * NW), 0, s, p, n_ct, n_tiles, 0);                                                     \
+    return;
+        DVIE_1X1_CE_CASE(0) DVIE_1X1_CE_CASE(1) DVIE_1X1_CE_CASE(2) DVIE_1X1_CE_CASE(3) DVIE_1X1_CE_CASE(4)
+        DVIE_1X1_CE_CASE(5) DVIE_1X1_CE_CASE(6) DVIE_1X1_CE_CASE(7)
+#undef DVIE_1X1_CE_CASE
+      }
     }
   }
   switch (pre) {

@@ -1284,7 +1284,6 @@ static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_nk_kernel<CP8, false>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
 }
 
-// DVIE_CONV_NK=0: narrow-input 3x3 convs on the chunked kernels (A/B runs)
 // ---------------------------------------------------------------------------------------
 // Eight-row halo tiles (conv_h8_kernel): stride-1 3x3 convs with c % 32 == 0 and
 // cout % 128 == 0 -- HRNet's 128- and 256-channel branch convs and their data gradients.
@@ -1541,8 +1540,9 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
       const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
           (void*)((const bf16_t*)p.z + ((EPI & 4) ? pix0 * p.z_ld : 0)), 0, 0x7FFFFFF0, 0x00020000);
       i32x4 o_r[2][2], o_b[2][2], o_z[2][2];  // [buffer][P]
+      // group gi: row r = gi >> 2, pixel half b = (gi >> 1) & 1, channel block i = gi & 1
       auto epi_load = [&](int gi) {
-        const int i = gi >> 2, r = (gi >> 1) & 1, b = gi & 1, u = gi & 1;
+        const int i = gi & 1, r = gi >> 2, b = (gi >> 1) & 1, u = gi & 1;
 #pragma unroll
           for (int P = 0; P < 2; ++P) {
             const int oy = J.y0 + 2 * wp + r, ox = J.x0 + 32 * b + r32;
@@ -1557,7 +1557,7 @@ __global__ __launch_bounds__(512) void conv_h8_kernel(const dvie_conv_desc p, in
       if (EPI) epi_load(0);
 #pragma unroll
       for (int gi = 0; gi < 8; ++gi) {
-        const int i = gi >> 2, r = (gi >> 1) & 1, b = gi & 1, u = gi & 1;
+        const int i = gi & 1, r = gi >> 2, b = (gi >> 1) & 1, u = gi & 1;
         if (EPI && gi < 7) epi_load(gi + 1);
         __builtin_amdgcn_sched_barrier(0);
         {
@@ -1657,6 +1657,7 @@ static bool conv_h8_launch(const dvie_conv_desc& p, hipStream_t s) {
   return true;
 }
 
+// DVIE_CONV_NK=0: narrow-input 3x3 convs on the chunked kernels (A/B runs)
 static const bool nk_env_off = getenv("DVIE_CONV_NK") && *getenv("DVIE_CONV_NK") == '0';
 
 bool conv_narrow_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_narrow.hip

@@ -100,7 +100,7 @@ __device__ __forceinline__ float warp_blend(float a, float b, float c, float d, 
 // Forward: a wave covers 256 consecutive pixels of one row, 4 per lane 64 apart: each gather
 // instruction reads the sources of 64 consecutive output pixels (a few cache lines for a
 // smooth flow), and the flow loads and output stores are 256-byte coalesced runs.
-template <int CC>
+template <int CC, int LAUX = 0, int SAUX = 0>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
   const int segs = (p.w + 255) >> 8;
   const long long hw = (long long)p.h * p.w;
@@ -121,8 +121,8 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
       const int x = (sg << 8) + lane + 64 * k;
       live[k] = x < p.w;
       const unsigned fo = (unsigned)(y * p.w + (live[k] ? x : p.w - 1)) * 4u;  // clamped: loads stay unconditional
-      fx[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf0, fo, 0, 0));
-      fy[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf1, fo, 0, 0));
+      fx[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf0, fo, 0, LAUX));
+      fy[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf1, fo, 0, LAUX));
     }
     WarpTap t[4];
 #pragma unroll
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {  // columns past the row end: out-of-range offset, store dropped
         const unsigned off = live[k] ? (unsigned)(y * p.w + (sg << 8) + lane + 64 * k) * 4u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[k]), out, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[k]), out, off, 0, SAUX);
       }
     };
     if constexpr (CC > 0) {
@@ -532,8 +532,21 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->out && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
   const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
   DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
-  const int grid = grid_for(waves * 256);
-  if (d->c == 3)
+  int grid = grid_for(waves * 256);
+  if (const char* e = getenv("DVIE_WARP_FWD_GRID")) {  // A/B: blocks = min(jobs / 4, cap)
+    const long long need = (waves + 3) / 4, cap = atoi(e);
+    if (cap > 0) grid = (int)(need < cap ? need : cap);
+  }
+  // flow loads and output stores read / written once: non-temporal (aux 2).  Same box,
+  // 8x3x256x512 8.2 -> 7.4 us, 8x3x1024x2048 128.9 -> 121.5 us (profiles/r04warpnt/).
+  // DVIE_WARP_NT (A/B, read per launch): 0 = default policy, 1 = non-temporal stores only
+  const char* nt = getenv("DVIE_WARP_NT");
+  const int ntm = nt && *nt ? atoi(nt) : 2;
+  if (d->c == 3 && ntm == 1)
+    hipLaunchKernelGGL((warp_fwd_kernel<3, 0, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+  else if (d->c == 3 && ntm == 2)
+    hipLaunchKernelGGL((warp_fwd_kernel<3, 2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+  else if (d->c == 3)
     hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
   else
     hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
@@ -724,7 +737,7 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
       case DVIE_OP_COLSUM: rc = dvie_colsum(&o.u.colsum, s); break;
       case DVIE_OP_EW: rc = dvie_ew(&o.u.ew, s); break;
       case DVIE_OP_LOSS: rc = dvie_loss(&o.u.loss, s); break;
-      case DVIE_OP_PACK: rc = dvie_pack_weights(o.u.pack.descs_dev, o.u.pack.n, o.u.pack.max_elems, s); break;
+      case DVIE_OP_PACK: rc = dvie_pack_weights(o.u.pack.descs_dev, o.u.pack.n, o.u.pack.blocks, s); break;
       case DVIE_OP_BN_FWD: rc = dvie_bn_fwd(&o.u.bn, s); break;
       case DVIE_OP_BN_BWD: rc = dvie_bn_bwd(&o.u.bn, s); break;
       case DVIE_OP_HEAD_FWD: rc = dvie_head_fwd(&o.u.head, s); break;

@@ -1651,6 +1651,10 @@ class Plan:
             self.bwd_arr = (L.Op * max(1, len(self.bwd)))(*self.bwd) if self.bwd else None
             self.n_bwd = len(self.bwd)
             return
+        blk = 0  # flat grid: each descriptor's first block of 1024 elements
+        for d in descs:
+            d.blk0 = blk
+            blk += -(-d.rows * d.kpad // 1024)
         arr = (L.PackDesc * len(descs))(*descs)
         raw = bytes(arr)
         dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
@@ -1658,7 +1662,7 @@ class Plan:
         po = self._op(L.OP_PACK)
         po.u.pack.descs_dev = dev.data_ptr()
         po.u.pack.n = len(descs)
-        po.u.pack.max_elems = max(d.rows * d.kpad for d in descs)
+        po.u.pack.blocks = blk
         self.fwd_arr = (L.Op * (len(self.fwd) + 1))(po, *self.fwd)
         self.fwd_off = 1
         self.bwd_arr = (L.Op * max(1, len(self.bwd)))(*self.bwd) if self.bwd else None

@@ -161,7 +161,10 @@ int dvie_colsum(const dvie_colsum_desc* d, void* stream);
  * mode 1 (transpose): dst[r][t*c + j] = src[j][cmap[r]][kh(t)][kw(t)], j < cout_s
  * with kh(t) = kh0 + (t / tw)*dkh, kw(t) = kw0 + (t % tw)*dkw; entries whose source is
  * out of range (cmap < 0, r/j past the source extent, k >= taps*c) are zero.
- * `n` descriptors are processed by one launch (descs points to DEVICE memory).
+ * `n` descriptors are processed by one launch (descs points to DEVICE memory) over a flat
+ * grid of `blocks` workgroups of 1024 elements: descriptor i owns blocks
+ * [blk0_i, blk0_i + ceil(rows_i * kpad_i / 1024)), the blk0 increasing with i (the caller
+ * fills them; `blocks` is the sum).
  */
 typedef struct dvie_pack_desc {
   const float* src;
@@ -170,10 +173,10 @@ typedef struct dvie_pack_desc {
   int rows, kpad, c, mode;
   int th, tw, kh0, kw0;
   int dkh, dkw, cout_s, cin_s;
-  int kh_s, kw_s, dtype, pad0;
+  int kh_s, kw_s, dtype, blk0; /* blk0: first flat-grid block of this descriptor */
 } dvie_pack_desc;
 
-int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int max_elems, void* stream);
+int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int blocks, void* stream);
 
 /*
  * Pointwise NHWC family (4 channels per thread).  op selects:
@@ -663,7 +666,7 @@ int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream);
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
-  int n, max_elems;
+  int n, blocks; /* dvie_pack_weights arguments */
 } dvie_pack_list;
 
 typedef struct dvie_op {

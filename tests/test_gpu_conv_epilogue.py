@@ -167,3 +167,53 @@ def test_conv_h8_modes(dev, shape, mode, monkeypatch):
         monkeypatch.setenv("DVIE_CONV_H8", env)
         errs[env] = _run(dev, shape, mode)
     assert errs["1"] < 1e-2 and errs["0"] < 1e-2, (shape, mode, errs)
+
+
+def _run_out(dev, shape, mode):
+    """the bf16 output tensor of _run's launch (same seeded operands)"""
+    n, H, W, c, cout, k = shape
+    g = torch.Generator().manual_seed(7)
+    x = _bf(torch.randn(n, H, W, c, generator=g))
+    wt = _bf(torch.randn(cout, c, k, k, generator=g) / (c * k * k) ** 0.5)
+    bias = torch.randn(cout, generator=g) * 0.1
+    res = _bf(torch.randn(n, H, W, cout, generator=g)) if "res" in mode else None
+    yold = _bf(torch.randn(n, H, W, cout, generator=g)) if "beta" in mode else None
+    z = _bf(torch.randn(n, H, W, cout, generator=g)) if "z" in mode else None
+    act = L.ACT_LRELU if mode in ("none", "res", "beta") else L.ACT_NONE
+    K = k * k * c
+    kpad = (K + 63) // 64 * 64
+    wp = torch.zeros(cout, kpad)
+    wp[:, :K] = wt.permute(0, 2, 3, 1).reshape(cout, K)
+    xd, wd, bd = x.to(torch.bfloat16).to(dev), wp.to(torch.bfloat16).to(dev), bias.to(dev)
+    yd = (yold if yold is not None else torch.zeros(n, H, W, cout)).to(torch.bfloat16).to(dev)
+    rd = res.to(torch.bfloat16).to(dev) if res is not None else None
+    zd = z.to(torch.bfloat16).to(dev) if z is not None else None
+    d = L.ConvDesc()
+    d.x, d.w, d.y, d.bias = xd.data_ptr(), wd.data_ptr(), yd.data_ptr(), bd.data_ptr()
+    d.res = rd.data_ptr() if rd is not None else None
+    d.z = zd.data_ptr() if zd is not None else None
+    d.x_ld, d.y_ld, d.res_ld, d.z_ld = c, cout, cout, cout
+    d.n, d.ih, d.iw, d.c, d.kpad, d.cout = n, H, W, c, kpad, cout
+    d.oh, d.ow, d.sy, d.sx = H, W, 1, 1
+    d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = k, k, -(k // 2), -(k // 2), 1, 1
+    d.yh, d.yw, d.osy, d.osx, d.ory, d.orx = H, W, 1, 1, 0, 0
+    d.act, d.dact, d.beta = act, L.ACT_LRELU if z is not None else L.ACT_NONE, int(yold is not None)
+    d.dtype, d.out_f32, d.alpha = L.BF16, 0, 0.2
+    L.check(L.load().dvie_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+            "conv")
+    torch.cuda.synchronize()
+    return yd.cpu()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", [(2, 37, 77, 64, 256, 1), (1, 33, 65, 64, 256, 1), (4, 64, 128, 64, 256, 1)])
+def test_conv_1x1_coalesced_epilogue_bit_exact(dev, shape, mode, monkeypatch):
+    """Single-K-step wide 1x1 (64 -> 256): the epilogue whose packed outputs are transposed
+    across 8-lane groups before the stores (DVIE_1X1_CE, default) writes the same bits as the
+    MFMA-layout stores, ragged last pixel tiles included."""
+    out = {}
+    for env in ("1", "0"):
+        monkeypatch.setenv("DVIE_1X1_CE", env)
+        out[env] = _run_out(dev, shape, mode)
+    assert torch.equal(out["1"], out["0"]), (shape, mode)
+

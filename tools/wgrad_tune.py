@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 from deep_video_interpolation_extrapolation_amd import _lib as L  # noqa: E402
 
+if os.environ.get("DVIE_TOOL_LIB"):  # e.g. a -DDVIE_TIMING_DBG build for DVIE_WG_DBG ablations
+    L.LIB_PATH = os.environ["DVIE_TOOL_LIB"]
+
 SHAPES = [  # name, cin, cout, k, H, W, batch
     ("3x3 64->64 256x512", 64, 64, 3, 256, 512, 8),
     ("3x3 128->128 128x256", 128, 128, 3, 128, 256, 8),
@@ -35,7 +38,7 @@ def main():
     dev = torch.device("cuda:0")
     s = L.stream_ptr()
     for name, cin, cout, k, H, W, B in SHAPES:
-        if only and only not in name:
+        if only and not any(o in name for o in only.split("|")):
             continue
         torch.manual_seed(0)
         x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
