@@ -59,9 +59,8 @@ def parse():
                          "1, hipGraph-captured step)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1: time the hipGraph-captured step (runners/graph.py), 0: the eager step; default 0 for "
-                         "c2 (same box, r03q: eager 216.4 vs captured 211.7 frames/s -- the graph replay runs the "
-                         "executor's side-stream lanes one after the other), 1 for c5 (the config names a "
-                         "captured step)")
+                         "c2 (same box, r04v: eager 34.9 ms with the executor's weight lane vs 35.4 ms captured -- "
+                         "a capture keeps every op on one stream), 1 for c5 (the config names a captured step)")
     return ap.parse_args()
 
 

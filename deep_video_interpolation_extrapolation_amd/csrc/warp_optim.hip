@@ -696,7 +696,13 @@ extern "C" {
 int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
   LaneRun lr;
   lr.main = (hipStream_t)stream;
-  const bool lanes = lanes_on();
+  // Under stream capture every op stays on the caller's stream: the weight lane's per-run
+  // waits become graph edges, and the replayed graph ran 23-33% slower than the one-stream
+  // capture (C2 43.7 vs 35.4 ms, C5 224 vs 169 ms per step, profiles/r04v/); eagerly the lane
+  // still gains (C2 34.9 vs 35.4 ms).
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(lr.main, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+  const bool lanes = lanes_on() && !capturing;
   auto finish = [&](int rc) {
     if (lr.d) {
       const hipError_t e = lr.finish();
