@@ -13,7 +13,11 @@
 // live in channel m*wh*ww + k.  Out-of-image neighbours are zero (the reference's zero
 // F.pad).  Every op ends with the engine's common epilogue:
 //   v += res; v += y_old (beta); v = act(v); v *= act'(z) (dact); y = v.
+#include <stdlib.h>
+
 #include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace dvie {
 
@@ -526,9 +530,216 @@ __global__ __launch_bounds__(256) void attn_gather_t_tile_kernel(const dvie_attn
   }
 }
 
+
+// ---- GATHER on the matrix cores (bf16, c % 32 == 0, windows up to 5 x 9) ----
+// For window row r and map m the tile's output is a band GEMM over the staged source row
+//   y[p][ch] += sum_s W[p][s] * B[s][ch],   s = source column - (x0 - rw), 0 <= s < 64 + 2 rw,
+//   W[p][s] = a[p][(half0 + m) K + r ww + (s - p)] for 0 <= s - p < ww, else 0,
+// computed as D[ch][p] = B^T[ch][s] W^T[s][p] with v_mfma_f32_32x32x16_bf16: the A operand
+// (32 channels x 16 sources) by transposed reads (ds_read_b64_tr_b16) of the staged rows, the
+// B operand (16 sources x 32 pixels) by plain reads of the band image, whose zero entries are
+// written once per workgroup (only the band positions are rewritten per window row).  A
+// 32-pixel block's band spans 40 sources: 3 k-steps.  The VALU form (attn_gather_tile_kernel)
+// reads every source value from LDS once per window column (9x); here the matrix cores do the
+// 9-tap sums, so the LDS traffic per output drops ~3x and the window sums leave the VALU.
+// Same products (bf16 x bf16 is exact in fp32); fp32 sums in another order.
+constexpr int GM_TP = 64, GM_SP = 80, GM_BP = 176;  // tile pixels, staged sources, band row pitch (B)
+
+__device__ __forceinline__ bf16x8 gm_tr_pair(const char* p0, const char* p1) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)p0);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)p1);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// TR: GATHER_T (the adjoint in b, one map): the band entry (q, s) is the weight of window
+// entry ((wh - 1 - r), q - s + 2 rw) stored at the SOURCE pixel s, so the band is built from
+// the source pixels' weight rows instead of the output pixels'.
+template <bool TR>
+__global__ __launch_bounds__(256) void attn_gather_mfma_kernel(const dvie_attn_desc p) {
+  __shared__ __attribute__((aligned(16))) char sB[2 * GM_SP * 128];   // [m][s][64 ch], chunks swizzled
+  __shared__ __attribute__((aligned(16))) char sW[2 * GM_TP * GM_BP]; // [m][p][s] band, bf16
+  const Tile t = tile_of(p.w, p.h);
+  const int K = p.wh * p.ww, rh = p.wh / 2, rw = p.ww / 2;
+  const int nm = p.b1 ? 2 : 1;
+  const bf16_t* maps[2] = {(const bf16_t*)p.b0, (const bf16_t*)p.b1};
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pb = wave & 1, cb = wave >> 1;  // 32-pixel block, 32-channel block of the chunk
+  const int r32 = lane & 31, hh = lane >> 5;
+  const long long pix0 = ((long long)t.n * p.h + t.y) * p.w + t.x0;
+  const int npx = min(GM_TP, p.w - t.x0);
+
+  for (int i = tid; i < 2 * GM_TP * GM_BP / 16; i += 256) ((i32x4*)sW)[i] = i32x4{0, 0, 0, 0};
+
+  // transposed-read addressing: lane 4 q + pq of 16-lane group g4 reads source row q (+4 for
+  // the second read, +8 for the upper half-wave) and 8 bytes at channel 16 (g4 & 1) + 4 pq of
+  // the wave's 32 channels; the chunk swizzle c ^ 4 ((s >> 1) & 1) keeps the reads conflict-free
+  const int g4 = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int tcol = 32 * cb + 16 * (g4 & 1) + 4 * tp;
+  const int a_off = (tq + 8 * (g4 >> 1)) * 128 + ((((tcol >> 3) ^ (((tq >> 1) & 1) << 2))) << 4) + (tcol & 7) * 2;
+  const int b_off = (32 * pb + r32) * GM_BP + hh * 16;
+
+  for (int c0 = 0; c0 < p.c; c0 += 64) {
+    f32x16 acc = {};
+    for (int r = 0; r < p.wh; ++r) {
+      const int yy = t.y + r - rh;
+      __syncthreads();  // the previous window row's MFMAs are done with sB / sW
+      for (int m = 0; m < nm; ++m) {
+        // source row segment: s -> column x0 - rw + s, 64 channels from c0 (zero outside)
+        for (int i = tid; i < GM_SP * 8; i += 256) {
+          const int s = i >> 3, ck = i & 7;
+          const int x = t.x0 - rw + s, ch = c0 + 8 * ck;
+          i32x4 v = {0, 0, 0, 0};
+          if (s < GM_TP + 2 * rw && (unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w && ch < p.c)
+            v = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
+          *(i32x4*)(sB + m * GM_SP * 128 + s * 128 + ((ck ^ (((s >> 1) & 1) << 2)) << 4)) = v;
+        }
+        if constexpr (!TR) {
+          // band values of this window row: W[q][q + kc] = a[q][(half0 + m) K + r ww + kc]
+          for (int i = tid; i < GM_TP * p.ww; i += 256) {
+            const int q = i / p.ww, kc = i - q * p.ww;
+            if (q < npx)
+              *(bf16_t*)(sW + m * GM_TP * GM_BP + q * GM_BP + (q + kc) * 2) =
+                  ((const bf16_t*)p.a)[(pix0 + q) * p.a_ld + (p.half0 + m) * K + r * p.ww + kc];
+          }
+        } else {
+          // W[q][s] = a[source s][half0 K + (wh - 1 - r) ww + kc], q = s - 2 rw + kc; sources
+          // outside the image are zero rows of sB, so their (stale, finite) band entries add 0
+          if ((unsigned)yy < (unsigned)p.h) {
+            for (int i = tid; i < (GM_TP + 2 * rw) * p.ww; i += 256) {
+              const int sx = i / p.ww, kc = i - sx * p.ww;
+              const int q = sx - 2 * rw + kc, x = t.x0 - rw + sx;
+              if (q >= 0 && q < npx && (unsigned)x < (unsigned)p.w)
+                *(bf16_t*)(sW + q * GM_BP + sx * 2) =
+                    ((const bf16_t*)p.a)[(((long long)t.n * p.h + yy) * p.w + x) * p.a_ld + p.half0 * K +
+                                         (p.wh - 1 - r) * p.ww + kc];
+            }
+          }
+        }
+      }
+      __syncthreads();
+      for (int m = 0; m < nm; ++m) {
+        const char* B = sB + m * GM_SP * 128;
+        const char* W = sW + m * GM_TP * GM_BP;
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          const int s0 = 32 * pb + 16 * ks;
+          const bf16x8 av = gm_tr_pair(B + a_off + s0 * 128, B + a_off + (s0 + 4) * 128);
+          const i32x4 bv = *(const i32x4*)(W + b_off + s0 * 2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+        }
+      }
+    }
+    // epilogue: permlane32 pairing -> 8 consecutive channels of one pixel per lane
+    float v[2][8];
+#pragma unroll
+    for (int P = 0; P < 2; ++P)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[8 * P + e]), __float_as_uint(acc[8 * P + 4 + e]),
+                                                         false, false);
+        v[P][e] = __uint_as_float(sw[0]);
+        v[P][4 + e] = __uint_as_float(sw[1]);
+      }
+    const int q = 32 * pb + r32;
+    if (q < npx) {
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        const int ch = c0 + 32 * cb + 16 * P + 8 * hh;
+        if (ch < p.c) {
+          epi4<bf16_t>(p, pix0 + q, ch, f32x4{v[P][0], v[P][1], v[P][2], v[P][3]});
+          epi4<bf16_t>(p, pix0 + q, ch + 4, f32x4{v[P][4], v[P][5], v[P][6], v[P][7]});
+        }
+      }
+    }
+  }
+}
+
+
+// ---- CORR on the matrix cores (bf16, c % 32 == 0, windows up to 5 x 9) ----
+// y[p][m K + r ww + kc] = <a[p], b_m[p + (r - rh, kc - rw)]>: for map m and window row r,
+// D[s][p] = sum_c B[s][c] a[p][c] over the staged source row (s = source column - (x0 - rw))
+// with v_mfma_f32_32x32x16_bf16 (A operand: source rows, B operand: the tile's pixels, both
+// plain row reads of XOR-swizzled 128-B rows), of which each lane keeps its band entries
+// s - p in [0, ww) and adds them into an fp32 LDS row per pixel (channels go in chunks of
+// 64).  Wave (pb, sb): pixel block pb, source block 32 pb + 32 sb .. +31.
+constexpr int CM_TP = 64, CM_SP = 80, CM_J = 2 * WHX * WWX;
+
+__global__ __launch_bounds__(256) void attn_corr_mfma_kernel(const dvie_attn_desc p) {
+  __shared__ __attribute__((aligned(16))) char sA[CM_TP * 128];
+  __shared__ __attribute__((aligned(16))) char sB[CM_SP * 128];
+  __shared__ float sO[CM_TP * CM_J];
+  const Tile t = tile_of(p.w, p.h);
+  const int K = p.wh * p.ww, rh = p.wh / 2, rw = p.ww / 2, J = p.nhalf * K;
+  const bf16_t* maps[2] = {(const bf16_t*)p.b0, (const bf16_t*)p.b1};
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pb = wave & 1, sb = wave >> 1;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const long long pix0 = ((long long)t.n * p.h + t.y) * p.w + t.x0;
+  const int npx = min(CM_TP, p.w - t.x0);
+  for (int i = tid; i < CM_TP * CM_J; i += 256) sO[i] = 0.f;
+
+  // this lane's operand rows; source rows past the staged 80 (pixel block 1, source block 1,
+  // lanes >= 16) read row 79: their entries are never in a band (s - p >= 17)
+  const int srow = min(32 * pb + 32 * sb + r32, CM_SP - 1), prow = 32 * pb + r32;
+  for (int c0 = 0; c0 < p.c; c0 += 64) {
+    __syncthreads();  // the previous chunk's reads of sA are done
+    for (int i = tid; i < CM_TP * 8; i += 256) {
+      const int q = i >> 3, ck = i & 7, ch = c0 + 8 * ck;
+      i32x4 v = {0, 0, 0, 0};
+      if (q < npx && ch < p.c) v = *(const i32x4*)((const bf16_t*)p.a + (pix0 + q) * p.a_ld + ch);
+      *(i32x4*)(sA + q * 128 + ((ck ^ ((q >> 1) & 7)) << 4)) = v;
+    }
+    for (int m = 0; m < p.nhalf; ++m) {
+      if (!maps[m]) continue;  // (uniform) a missing map's entries stay zero
+      for (int r = 0; r < p.wh; ++r) {
+        const int yy = t.y + r - rh;
+        __syncthreads();  // sA staged / the previous window row's reads of sB are done
+        for (int i = tid; i < CM_SP * 8; i += 256) {
+          const int s = i >> 3, ck = i & 7;
+          const int x = t.x0 - rw + s, ch = c0 + 8 * ck;
+          i32x4 v = {0, 0, 0, 0};
+          if (s < CM_TP + 2 * rw && (unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w && ch < p.c)
+            v = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
+          *(i32x4*)(sB + s * 128 + ((ck ^ ((s >> 1) & 7)) << 4)) = v;
+        }
+        __syncthreads();
+        f32x16 acc = {};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int ck = 2 * ks + hh;
+          const i32x4 av = *(const i32x4*)(sB + srow * 128 + ((ck ^ ((srow >> 1) & 7)) << 4));
+          const i32x4 bv = *(const i32x4*)(sA + prow * 128 + ((ck ^ ((prow >> 1) & 7)) << 4));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv),
+                                                        acc, 0, 0, 0);
+        }
+        // lane: pixel prow (column), sources 32 pb + 32 sb + 8 (e / 4) + 4 hh + e % 4 (rows)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int s = 32 * pb + 32 * sb + 8 * (e >> 2) + 4 * hh + (e & 3);
+          const int kc = s - prow;
+          if (kc >= 0 && kc < p.ww) sO[prow * CM_J + m * K + r * p.ww + kc] += acc[e];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < npx * J; e += 256) {
+    const int q = e / J, j = e - q * J;
+    epi1<bf16_t>(p, pix0 + q, j, sO[q * CM_J + j]);
+  }
+}
+
 }  // namespace dvie
 
 using namespace dvie;
+
+// DVIE_ATTN_MFMA=0: the VALU window kernels for GATHER / GATHER_T / CORR (A/B runs); read per launch
+static bool gm_on() {
+  const char* e = getenv("DVIE_ATTN_MFMA");
+  return !(e && *e == '0');
+}
 
 extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->a && d->y, "attn: null pointer");
@@ -559,6 +770,14 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
                        "attn: gather half0=%d nhalf=%d", d->half0, d->nhalf);
         DVIE_CHECK_ARG(d->op == DVIE_ATTN_GATHER || !d->b1, "attn: gather_t takes one map");
       }
+      if ((d->op == DVIE_ATTN_GATHER || d->op == DVIE_ATTN_GATHER_T) && tiled && bf && d->c % 32 == 0 &&
+          d->b_ld % 8 == 0 && gm_on()) {
+        if (d->op == DVIE_ATTN_GATHER)
+          hipLaunchKernelGGL(attn_gather_mfma_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        else
+          hipLaunchKernelGGL(attn_gather_mfma_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        break;
+      }
       if (tiled && d->op == DVIE_ATTN_GATHER) {
         if (bf)
           hipLaunchKernelGGL(attn_gather_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
@@ -585,6 +804,10 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
       DVIE_CHECK_ARG((d->nhalf == 1 || d->nhalf == 2) && (d->b0 || d->b1), "attn: corr maps");
       DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0, "attn: corr c=%d", d->c);
       DVIE_CHECK_ARG(d->y_ld >= d->nhalf * K, "attn: corr y_ld");
+      if (tiled && bf && d->c % 32 == 0 && d->a_ld % 8 == 0 && d->b_ld % 8 == 0 && gm_on()) {
+        hipLaunchKernelGGL(attn_corr_mfma_kernel, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        break;
+      }
       if (tiled) {
         if (bf)
           hipLaunchKernelGGL(attn_corr_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
