@@ -580,57 +580,84 @@ __global__ __launch_bounds__(256) void attn_gather_mfma_kernel(const dvie_attn_d
   const int a_off = (tq + 8 * (g4 >> 1)) * 128 + ((((tcol >> 3) ^ (((tq >> 1) & 1) << 2))) << 4) + (tcol & 7) * 2;
   const int b_off = (32 * pb + r32) * GM_BP + hh * 16;
 
-  for (int c0 = 0; c0 < p.c; c0 += 64) {
-    f32x16 acc = {};
-    for (int r = 0; r < p.wh; ++r) {
-      const int yy = t.y + r - rh;
-      __syncthreads();  // the previous window row's MFMAs are done with sB / sW
-      for (int m = 0; m < nm; ++m) {
-        // source row segment: s -> column x0 - rw + s, 64 channels from c0 (zero outside)
-        for (int i = tid; i < GM_SP * 8; i += 256) {
-          const int s = i >> 3, ck = i & 7;
-          const int x = t.x0 - rw + s, ch = c0 + 8 * ck;
-          i32x4 v = {0, 0, 0, 0};
-          if (s < GM_TP + 2 * rw && (unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w && ch < p.c)
-            v = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
-          *(i32x4*)(sB + m * GM_SP * 128 + s * 128 + ((ck ^ (((s >> 1) & 1) << 2)) << 4)) = v;
-        }
-        if constexpr (!TR) {
-          // band values of this window row: W[q][q + kc] = a[q][(half0 + m) K + r ww + kc]
-          for (int i = tid; i < GM_TP * p.ww; i += 256) {
-            const int q = i / p.ww, kc = i - q * p.ww;
-            if (q < npx)
-              *(bf16_t*)(sW + m * GM_TP * GM_BP + q * GM_BP + (q + kc) * 2) =
-                  ((const bf16_t*)p.a)[(pix0 + q) * p.a_ld + (p.half0 + m) * K + r * p.ww + kc];
-          }
-        } else {
-          // W[q][s] = a[source s][half0 K + (wh - 1 - r) ww + kc], q = s - 2 rw + kc; sources
-          // outside the image are zero rows of sB, so their (stale, finite) band entries add 0
-          if ((unsigned)yy < (unsigned)p.h) {
-            for (int i = tid; i < (GM_TP + 2 * rw) * p.ww; i += 256) {
-              const int sx = i / p.ww, kc = i - sx * p.ww;
-              const int q = sx - 2 * rw + kc, x = t.x0 - rw + sx;
-              if (q >= 0 && q < npx && (unsigned)x < (unsigned)p.w)
-                *(bf16_t*)(sW + q * GM_BP + sx * 2) =
-                    ((const bf16_t*)p.a)[(((long long)t.n * p.h + yy) * p.w + x) * p.a_ld + p.half0 * K +
-                                         (p.wh - 1 - r) * p.ww + kc];
-            }
-          }
-        }
-      }
-      __syncthreads();
-      for (int m = 0; m < nm; ++m) {
-        const char* B = sB + m * GM_SP * 128;
-        const char* W = sW + m * GM_TP * GM_BP;
+  // stages st = (channel chunk st / wh, window row st % wh); the next stage's source rows and
+  // band weights are loaded into registers while this stage's MFMAs run (3 workgroups per CU
+  // hide the rest), and written to LDS after the next barrier
+  const int nstage = ((p.c + 63) / 64) * p.wh;
+  i32x4 pv[2][3];
+  bf16_t pw[2][3];
+  auto fetch = [&](int st) {
+    const int c0 = 64 * (st / p.wh), r = st % p.wh, yy = t.y + r - rh;
 #pragma unroll
-        for (int ks = 0; ks < 3; ++ks) {
-          const int s0 = 32 * pb + 16 * ks;
-          const bf16x8 av = gm_tr_pair(B + a_off + s0 * 128, B + a_off + (s0 + 4) * 128);
-          const i32x4 bv = *(const i32x4*)(W + b_off + s0 * 2);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+    for (int m = 0; m < 2; ++m) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int i = tid + 256 * u, s = i >> 3, ck = i & 7;
+        const int x = t.x0 - rw + s, ch = c0 + 8 * ck;
+        pv[m][u] = i32x4{0, 0, 0, 0};
+        if (m < nm && i < GM_SP * 8 && s < GM_TP + 2 * rw && (unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w &&
+            ch < p.c)
+          pv[m][u] = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
+        pw[m][u] = 0;
+        if constexpr (!TR) {
+          const int q = i / p.ww, kc = i - q * p.ww;
+          if (m < nm && i < GM_TP * p.ww && q < npx)
+            pw[m][u] = ((const bf16_t*)p.a)[(pix0 + q) * p.a_ld + (p.half0 + m) * K + r * p.ww + kc];
+        } else {
+          const int sx = i / p.ww, kc = i - sx * p.ww, xs = t.x0 - rw + sx;
+          if (m == 0 && i < (GM_TP + 2 * rw) * p.ww && (unsigned)yy < (unsigned)p.h && (unsigned)xs < (unsigned)p.w)
+            pw[m][u] = ((const bf16_t*)p.a)[(((long long)t.n * p.h + yy) * p.w + xs) * p.a_ld + p.half0 * K +
+                                            (p.wh - 1 - r) * p.ww + kc];
         }
       }
     }
+  };
+  auto store = [&](int st) {
+    const int r = st % p.wh, yy = t.y + r - rh;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      if (m >= nm) continue;
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int i = tid + 256 * u, s = i >> 3, ck = i & 7;
+        if (i < GM_SP * 8) *(i32x4*)(sB + m * GM_SP * 128 + s * 128 + ((ck ^ (((s >> 1) & 1) << 2)) << 4)) = pv[m][u];
+        if constexpr (!TR) {
+          // band values of this window row: W[q][q + kc] = a[q][(half0 + m) K + r ww + kc]
+          const int q = i / p.ww, kc = i - q * p.ww;
+          if (i < GM_TP * p.ww && q < npx) *(bf16_t*)(sW + m * GM_TP * GM_BP + q * GM_BP + (q + kc) * 2) = pw[m][u];
+        } else {
+          // W[q][s] = a[source s][half0 K + (wh - 1 - r) ww + kc], q = s - 2 rw + kc; sources
+          // outside the image are zero rows of sB, so their (stale, finite) band entries add 0
+          const int sx = i / p.ww, kc = i - sx * p.ww, q = sx - 2 * rw + kc, xs = t.x0 - rw + sx;
+          if (m == 0 && i < (GM_TP + 2 * rw) * p.ww && q >= 0 && q < npx && (unsigned)yy < (unsigned)p.h &&
+              (unsigned)xs < (unsigned)p.w)
+            *(bf16_t*)(sW + q * GM_BP + sx * 2) = pw[m][u];
+        }
+      }
+    }
+  };
+
+  static_assert(GM_SP * 8 <= 3 * 256 && GM_TP * WWX <= 3 * 256 && (GM_TP + WWX - 1) * WWX <= 3 * 256, "prefetch slots");
+  fetch(0);
+  f32x16 acc = {};
+  for (int st = 0; st < nstage; ++st) {
+    const int c0 = 64 * (st / p.wh), r = st % p.wh;
+    __syncthreads();  // the previous stage's MFMAs are done with sB / sW
+    store(st);
+    if (st + 1 < nstage) fetch(st + 1);
+    __syncthreads();
+    for (int m = 0; m < nm; ++m) {
+      const char* B = sB + m * GM_SP * 128;
+      const char* W = sW + m * GM_TP * GM_BP;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int s0 = 32 * pb + 16 * ks;
+        const bf16x8 av = gm_tr_pair(B + a_off + s0 * 128, B + a_off + (s0 + 4) * 128);
+        const i32x4 bv = *(const i32x4*)(W + b_off + s0 * 2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+      }
+    }
+    if (r + 1 < p.wh) continue;
     // epilogue: permlane32 pairing -> 8 consecutive channels of one pixel per lane
     float v[2][8];
 #pragma unroll
@@ -653,6 +680,7 @@ __global__ __launch_bounds__(256) void attn_gather_mfma_kernel(const dvie_attn_d
         }
       }
     }
+    acc = f32x16{};
   }
 }
 
@@ -683,45 +711,70 @@ __global__ __launch_bounds__(256) void attn_corr_mfma_kernel(const dvie_attn_des
   // this lane's operand rows; source rows past the staged 80 (pixel block 1, source block 1,
   // lanes >= 16) read row 79: their entries are never in a band (s - p >= 17)
   const int srow = min(32 * pb + 32 * sb + r32, CM_SP - 1), prow = 32 * pb + r32;
-  for (int c0 = 0; c0 < p.c; c0 += 64) {
-    __syncthreads();  // the previous chunk's reads of sA are done
-    for (int i = tid; i < CM_TP * 8; i += 256) {
-      const int q = i >> 3, ck = i & 7, ch = c0 + 8 * ck;
-      i32x4 v = {0, 0, 0, 0};
-      if (q < npx && ch < p.c) v = *(const i32x4*)((const bf16_t*)p.a + (pix0 + q) * p.a_ld + ch);
-      *(i32x4*)(sA + q * 128 + ((ck ^ ((q >> 1) & 7)) << 4)) = v;
+  // stages st = (channel chunk, live map, window row); the next stage's source row (and at a
+  // chunk's first stage its pixel rows) are loaded into registers while this stage's MFMAs run
+  // live maps (a missing map's entries stay zero): lm0, and lm1 when both are present
+  const int nlive = (p.b0 ? 1 : 0) + (p.nhalf > 1 && p.b1 ? 1 : 0);
+  const int lm0 = p.b0 ? 0 : 1, lm1 = 1;
+  const int per_chunk = nlive * p.wh, nstage = ((p.c + 63) / 64) * per_chunk;
+  i32x4 pv[3], pa[2];
+  auto fetch = [&](int st) {
+    const int c0 = 64 * (st / per_chunk), rem = st % per_chunk, m = rem / p.wh ? lm1 : lm0, r = rem % p.wh;
+    const int yy = t.y + r - rh;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int i = tid + 256 * u, s = i >> 3, ck = i & 7;
+      const int x = t.x0 - rw + s, ch = c0 + 8 * ck;
+      pv[u] = i32x4{0, 0, 0, 0};
+      if (i < CM_SP * 8 && s < CM_TP + 2 * rw && (unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w && ch < p.c)
+        pv[u] = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
     }
-    for (int m = 0; m < p.nhalf; ++m) {
-      if (!maps[m]) continue;  // (uniform) a missing map's entries stay zero
-      for (int r = 0; r < p.wh; ++r) {
-        const int yy = t.y + r - rh;
-        __syncthreads();  // sA staged / the previous window row's reads of sB are done
-        for (int i = tid; i < CM_SP * 8; i += 256) {
-          const int s = i >> 3, ck = i & 7;
-          const int x = t.x0 - rw + s, ch = c0 + 8 * ck;
-          i32x4 v = {0, 0, 0, 0};
-          if (s < CM_TP + 2 * rw && (unsigned)yy < (unsigned)p.h && (unsigned)x < (unsigned)p.w && ch < p.c)
-            v = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
-          *(i32x4*)(sB + s * 128 + ((ck ^ ((s >> 1) & 7)) << 4)) = v;
-        }
-        __syncthreads();
-        f32x16 acc = {};
+    if (rem == 0) {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int ck = 2 * ks + hh;
-          const i32x4 av = *(const i32x4*)(sB + srow * 128 + ((ck ^ ((srow >> 1) & 7)) << 4));
-          const i32x4 bv = *(const i32x4*)(sA + prow * 128 + ((ck ^ ((prow >> 1) & 7)) << 4));
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv),
-                                                        acc, 0, 0, 0);
-        }
-        // lane: pixel prow (column), sources 32 pb + 32 sb + 8 (e / 4) + 4 hh + e % 4 (rows)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int s = 32 * pb + 32 * sb + 8 * (e >> 2) + 4 * hh + (e & 3);
-          const int kc = s - prow;
-          if (kc >= 0 && kc < p.ww) sO[prow * CM_J + m * K + r * p.ww + kc] += acc[e];
-        }
+      for (int u = 0; u < 2; ++u) {
+        const int i = tid + 256 * u, q = i >> 3, ck = i & 7, ch = c0 + 8 * ck;
+        pa[u] = i32x4{0, 0, 0, 0};
+        if (q < npx && ch < p.c) pa[u] = *(const i32x4*)((const bf16_t*)p.a + (pix0 + q) * p.a_ld + ch);
       }
+    }
+  };
+  auto store = [&](int st) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int i = tid + 256 * u, s = i >> 3, ck = i & 7;
+      if (i < CM_SP * 8) *(i32x4*)(sB + s * 128 + ((ck ^ ((s >> 1) & 7)) << 4)) = pv[u];
+    }
+    if (st % per_chunk == 0) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = tid + 256 * u, q = i >> 3, ck = i & 7;
+        *(i32x4*)(sA + q * 128 + ((ck ^ ((q >> 1) & 7)) << 4)) = pa[u];
+      }
+    }
+  };
+  static_assert(CM_SP * 8 <= 3 * 256 && CM_TP * 8 == 2 * 256, "prefetch slots");
+  if (nstage > 0) fetch(0);
+  for (int st = 0; st < nstage; ++st) {
+    const int rem = st % per_chunk, m = rem / p.wh ? lm1 : lm0, r = rem % p.wh;
+    __syncthreads();  // sO zeroed / the previous stage's reads of sA / sB are done
+    store(st);
+    if (st + 1 < nstage) fetch(st + 1);
+    __syncthreads();
+    f32x16 acc = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int ck = 2 * ks + hh;
+      const i32x4 av = *(const i32x4*)(sB + srow * 128 + ((ck ^ ((srow >> 1) & 7)) << 4));
+      const i32x4 bv = *(const i32x4*)(sA + prow * 128 + ((ck ^ ((prow >> 1) & 7)) << 4));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), acc,
+                                                    0, 0, 0);
+    }
+    // lane: pixel prow (column), sources 32 pb + 32 sb + 8 (e / 4) + 4 hh + e % 4 (rows)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int s = 32 * pb + 32 * sb + 8 * (e >> 2) + 4 * hh + (e & 3);
+      const int kc = s - prow;
+      if (kc >= 0 && kc < p.ww) sO[prow * CM_J + m * K + r * p.ww + kc] += acc[e];
     }
   }
   __syncthreads();

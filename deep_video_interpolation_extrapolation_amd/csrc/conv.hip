@@ -344,11 +344,41 @@ __global__ __launch_bounds__(256) void colsum_kernel(const dvie_colsum_desc p, l
   }
 }
 
-// Flat grid: block b belongs to the last descriptor whose blk0 <= b (uniform binary search);
-// a thread packs 4 consecutive elements of its descriptor (one 8-byte bf16 store when the
-// four share a row).  The earlier (block x, descriptor y) grid launched max-size x blocks for
-// every descriptor, nearly all of them empty: 0.29 ms per step for ~40 MB of weights.
+// Flat grid: block b belongs to the last descriptor whose blk0 <= b (uniform binary search).
+// Three block kinds, a pure function of the descriptor (pack_kind; engine.py pack_blocks
+// mirrors it):
+//   ROW  (mode 0, kpad >= 64): one packed row; its source row w[co][:][:][:] is contiguous,
+//        so it is staged in LDS by coalesced loads and the row written 4 elements per thread.
+//   TILE (mode 1, kpad >= 64): 8 packed rows (source channels) x 64 columns (output
+//        channels); the source block w[co0 .. +64][ci of the 8 rows][taps] is staged in LDS
+//        (contiguous per co), then every (row, tap) writes 64 consecutive columns.
+//   ELEM (the rest: biases, tiny layers): 1024 elements, 4 per thread.
+// The element-wise form alone gathered every source value with a 36 B (mode 0) or cin * 36 B
+// (mode 1) stride: 0.27 ms per step for ~40 MB of weights.
+enum { PACK_ELEM = 0, PACK_ROW = 1, PACK_TILE = 2 };
+constexpr int PACK_LDS = 8192;  // floats
+constexpr int PACK_TR = 8, PACK_TC = 64;
+
+__host__ __device__ inline int pack_kind(const dvie_pack_desc& d) {
+  if (d.kpad < 64 || d.kpad % 4 != 0) return PACK_ELEM;
+  if (d.mode == 0 && d.cin_s * d.kh_s * d.kw_s <= PACK_LDS) return PACK_ROW;
+  if (d.mode == 1 && d.kh_s * d.kw_s <= 16 && d.c % 4 == 0) return PACK_TILE;
+  return PACK_ELEM;
+}
+
+__device__ __forceinline__ void pack_store4(const dvie_pack_desc& p, long long e, const float* v) {
+  if (p.dtype == DVIE_BF16) {
+    uint2 u;
+    u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *(uint2*)((bf16_t*)p.dst + e) = u;
+  } else {
+    *(f32x4*)((float*)p.dst + e) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+
 __global__ __launch_bounds__(256) void pack_kernel(const dvie_pack_desc* __restrict__ descs, int n) {
+  __shared__ float lds[PACK_LDS];
   int lo = 0, hi = n - 1;
   const int b = blockIdx.x;
   while (lo < hi) {
@@ -359,10 +389,72 @@ __global__ __launch_bounds__(256) void pack_kernel(const dvie_pack_desc* __restr
       hi = mid - 1;
   }
   const dvie_pack_desc p = descs[lo];
+  const int lb = b - p.blk0;
+  const int ntap = p.th * p.tw, tid = threadIdx.x;
+  const int kind = pack_kind(p);
+
+  if (kind == PACK_ROW) {
+    // packed row r = output channel co: dst[r][t c + j] = w[r][cmap[j]][kh(t)][kw(t)]
+    const int r = lb, L = p.cin_s * p.kh_s * p.kw_s;
+    const bool live = r < p.cout_s;
+    for (int i = tid; i < L; i += 256) lds[i] = live ? p.src[(long long)r * L + i] : 0.f;
+    __syncthreads();
+    for (int k0 = 4 * tid; k0 < p.kpad; k0 += 1024) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = k0 + q, t = k / p.c, j = k - t * p.c;
+        v[q] = 0.f;
+        if (live && t < ntap) {
+          const int ci = p.cmap ? p.cmap[j] : j;
+          const int kh = p.kh0 + (t / p.tw) * p.dkh, kw = p.kw0 + (t % p.tw) * p.dkw;
+          if (ci >= 0 && ci < p.cin_s && kh >= 0 && kh < p.kh_s && kw >= 0 && kw < p.kw_s)
+            v[q] = lds[(ci * p.kh_s + kh) * p.kw_s + kw];
+        }
+      }
+      pack_store4(p, (long long)r * p.kpad + k0, v);
+    }
+    return;
+  }
+  if (kind == PACK_TILE) {
+    // rows r0 .. r0+7 (source channels cmap[r]), columns j0 .. j0+63 (output channels) of
+    // every tap: dst[r][t c + j] = w[j][cmap[r]][kh(t)][kw(t)]
+    const int ncb = (p.c + PACK_TC - 1) / PACK_TC;
+    const int r0 = (lb / ncb) * PACK_TR, j0 = (lb % ncb) * PACK_TC;
+    const int T = p.kh_s * p.kw_s;
+    for (int i = tid; i < PACK_TC * PACK_TR * T; i += 256) {  // lds[jj][k][tap], tap fastest
+      const int jj = i / (PACK_TR * T), rem = i - jj * (PACK_TR * T), k = rem / T, tp = rem - k * T;
+      const int co = j0 + jj, r = r0 + k;
+      const int ci = r < p.rows ? (p.cmap ? p.cmap[r] : r) : -1;
+      lds[i] = (co < p.cout_s && ci >= 0 && ci < p.cin_s) ? p.src[((long long)co * p.cin_s + ci) * T + tp] : 0.f;
+    }
+    __syncthreads();
+    const int nq = PACK_TC / 4;  // 4 consecutive columns per thread
+    for (int i = tid; i < PACK_TR * ntap * nq; i += 256) {
+      const int k = i / (ntap * nq), rem = i - k * (ntap * nq), t = rem / nq, jq = rem - t * nq;
+      const int r = r0 + k, j = j0 + 4 * jq;
+      if (r >= p.rows || j >= p.c) continue;
+      const int kh = p.kh0 + (t / p.tw) * p.dkh, kw = p.kw0 + (t % p.tw) * p.dkw;
+      const bool tap_ok = kh >= 0 && kh < p.kh_s && kw >= 0 && kw < p.kw_s;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = tap_ok ? lds[((j - j0 + q) * PACK_TR + k) * T + kh * p.kw_s + kw] : 0.f;
+      pack_store4(p, (long long)r * p.kpad + t * p.c + j, v);
+    }
+    if (j0 == 0) {  // the K padding [ntap c, kpad) of these rows
+      const int pad = p.kpad - ntap * p.c;
+      for (int i = tid; i < PACK_TR * (pad / 4); i += 256) {
+        const int k = i / (pad / 4), q4 = i - k * (pad / 4);
+        const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        if (r0 + k < p.rows) pack_store4(p, (long long)(r0 + k) * p.kpad + ntap * p.c + 4 * q4, z);
+      }
+    }
+    return;
+  }
+  // ELEM
   const long long total = (long long)p.rows * p.kpad;
-  const long long e0 = ((long long)(b - p.blk0) * 256 + threadIdx.x) * 4;
+  const long long e0 = ((long long)lb * 256 + tid) * 4;
   if (e0 >= total) return;
-  const int ntap = p.th * p.tw;
   float v[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -388,21 +480,14 @@ __global__ __launch_bounds__(256) void pack_kernel(const dvie_pack_desc* __restr
         v[q] = p.src[(((long long)co * p.cin_s + ci) * p.kh_s + kh) * p.kw_s + kw];
     }
   }
-  if (p.dtype == DVIE_BF16) {
-    bf16_t* d = (bf16_t*)p.dst + e0;
-    if (e0 + 4 <= total && p.kpad % 4 == 0) {  // four of one row, 8-byte aligned
-      uint2 u;
-      u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *(uint2*)d = u;
-    } else {
-      for (int q = 0; q < 4; ++q)
-        if (e0 + q < total) d[q] = f2bf(v[q]);
-    }
-  } else {
-    float* d = (float*)p.dst + e0;
+  if (e0 + 4 <= total && p.kpad % 4 == 0) {  // four of one row, aligned
+    pack_store4(p, e0, v);
+  } else if (p.dtype == DVIE_BF16) {
     for (int q = 0; q < 4; ++q)
-      if (e0 + q < total) d[q] = v[q];
+      if (e0 + q < total) ((bf16_t*)p.dst)[e0 + q] = f2bf(v[q]);
+  } else {
+    for (int q = 0; q < 4; ++q)
+      if (e0 + q < total) ((float*)p.dst)[e0 + q] = v[q];
   }
 }
 

@@ -35,6 +35,17 @@ def _wgrad_lane():
     return os.environ.get("DVIE_WGRAD_LANE", "1") != "0"
 
 
+def pack_blocks(d):
+    """workgroups dvie_pack_weights gives descriptor d: the kinds of csrc/conv.hip pack_kind
+    (ROW: one per packed row, TILE: 8 rows x 64 columns, ELEM: 1024 elements)"""
+    if d.kpad >= 64 and d.kpad % 4 == 0:
+        if d.mode == 0 and d.cin_s * d.kh_s * d.kw_s <= 8192:
+            return d.rows
+        if d.mode == 1 and d.kh_s * d.kw_s <= 16 and d.c % 4 == 0:
+            return -(-d.rows // 8) * -(-d.c // 64)
+    return -(-d.rows * d.kpad // 1024)
+
+
 def _reduce_meta(name, r):
     """profiling meta of a slab reduction: the partial slabs read once, the gradient
     written (and read when accumulating)."""
@@ -557,6 +568,8 @@ class Plan:
         self.keep = []  # tensors referenced by raw pointers
         self.busy = False
         self.generation = 0
+        self.static_weights = False  # set by owners whose weights never train (nets/vgg.py)
+        self._pack_srcs, self._pack_sig = [], None
         self._alloc()
         self.fwd = []
         self.bwd = []
@@ -646,6 +659,10 @@ class Plan:
     # ---------------- weight packing ----------------
     def _build_pack(self):
         descs = []
+        # the tensors the pack reads (static_weights plans repack only when one changed)
+        self._pack_srcs = [t for lay in self.g.layers if lay.cin_p is not None
+                           for t in (lay.m.weight, lay.m.bias if lay.has_bias else None) if t is not None]
+        self._pack_sig = None
         for lay in self.g.layers:
             if lay.cin_p is None:
                 continue
@@ -1651,10 +1668,10 @@ class Plan:
             self.bwd_arr = (L.Op * max(1, len(self.bwd)))(*self.bwd) if self.bwd else None
             self.n_bwd = len(self.bwd)
             return
-        blk = 0  # flat grid: each descriptor's first block of 1024 elements
+        blk = 0  # flat grid: each descriptor's first block (csrc/conv.hip pack_kernel)
         for d in descs:
             d.blk0 = blk
-            blk += -(-d.rows * d.kpad // 1024)
+            blk += pack_blocks(d)
         arr = (L.PackDesc * len(descs))(*descs)
         raw = bytes(arr)
         dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
@@ -1867,7 +1884,15 @@ class Plan:
     def run_forward(self, stream=None):
         s = L.stream_ptr() if stream is None else stream
         metas = [None] * self.fwd_off + [getattr(o, "meta", None) for o in self.fwd]
-        self._run(self.fwd_arr, 0, len(self.fwd_arr), s, "forward plan", metas)
+        start = 0
+        if self.fwd_off and self.static_weights:
+            # frozen weights (VGG19, the loss network): pack once, again only when a source
+            # tensor is replaced or modified in place (load_state_dict bumps its version)
+            sig = tuple((t.data_ptr(), t._version) for t in self._pack_srcs)
+            if sig == self._pack_sig:
+                start = self.fwd_off
+            self._pack_sig = sig
+        self._run(self.fwd_arr, start, len(self.fwd_arr), s, "forward plan", metas)
         self.generation += 1
 
     def run_backward(self, stream=None, cuts=(), on_cut=None):

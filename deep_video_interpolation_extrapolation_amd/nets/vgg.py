@@ -120,6 +120,7 @@ class my_vgg(nn.Module):
         g = E.Graph(dtype)
         feats = self.lower(g, H, W, normalize, loss)
         plan = g.compile(2 * n if loss else n, dev, n_bwd=n, backward=loss)
+        plan.static_weights = True  # frozen loss network: the weights are packed once
         plan.feats = feats
         return plan
 

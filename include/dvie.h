@@ -162,9 +162,11 @@ int dvie_colsum(const dvie_colsum_desc* d, void* stream);
  * with kh(t) = kh0 + (t / tw)*dkh, kw(t) = kw0 + (t % tw)*dkw; entries whose source is
  * out of range (cmap < 0, r/j past the source extent, k >= taps*c) are zero.
  * `n` descriptors are processed by one launch (descs points to DEVICE memory) over a flat
- * grid of `blocks` workgroups of 1024 elements: descriptor i owns blocks
- * [blk0_i, blk0_i + ceil(rows_i * kpad_i / 1024)), the blk0 increasing with i (the caller
- * fills them; `blocks` is the sum).
+ * grid of `blocks` workgroups: descriptor i owns blocks [blk0_i, blk0_i + nb_i), the blk0
+ * increasing with i (the caller fills them; `blocks` is the sum), with nb = rows (mode 0,
+ * kpad >= 64 and kpad % 4 == 0, cin_s*kh_s*kw_s <= 8192: one packed row per block),
+ * ceil(rows / 8) * ceil(c / 64) (mode 1, the same kpad, kh_s*kw_s <= 16, c % 4 == 0: 8 rows x
+ * 64 columns per block), else ceil(rows * kpad / 1024) (1024 elements per block).
  */
 typedef struct dvie_pack_desc {
   const float* src;

@@ -135,6 +135,30 @@ def test_vgg_loss(dev, prec, monkeypatch):
     assert rel_err(g, gr) < (1e-3 if prec == "fp32" else 1e-1)
 
 
+def test_vgg_repacks_changed_weights(dev, monkeypatch):
+    """The frozen VGG19 plan packs its weights once (Plan.static_weights); an in-place weight
+    update (new version counter) must be repacked: the loss after scaling features.0 by 2
+    equals a fresh module's with the scaled weights."""
+    monkeypatch.setenv("DVIE_PRECISION", "fp32")
+    from deep_video_interpolation_extrapolation_amd import losses as DL
+    pred, gt, _ = inputs.rgbloss_inputs()["pm1"]
+    pred, gt = pred.to(dev), gt.to(dev)
+    vl = DL.VGGLoss().to(dev)
+    a = float(vl(pred, gt, normed=False))
+    assert float(vl(pred, gt, normed=False)) == a  # skipped pack: same weights, same value
+    w = [p for n, p in vl.named_parameters() if n.endswith("features.0.weight")]
+    assert len(w) == 1
+    with torch.no_grad():
+        w[0].mul_(2)
+    b = float(vl(pred, gt, normed=False))
+    ref = DL.VGGLoss().to(dev)
+    w2 = [p for n, p in ref.named_parameters() if n.endswith("features.0.weight")][0]
+    with torch.no_grad():
+        w2.mul_(2)
+    c = float(ref(pred, gt, normed=False))
+    assert b != a and abs(b - c) <= 1e-6 * abs(c)
+
+
 def test_warp(dev):
     from deep_video_interpolation_extrapolation_amd.utils.net_utils import FlowWrapper
     x, flow, dout = inputs.warp_inputs()
