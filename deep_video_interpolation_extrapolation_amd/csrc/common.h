@@ -101,4 +101,20 @@ __device__ __forceinline__ float act_dz(float z, int act, float alpha) {
 
 __host__ __device__ __forceinline__ int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// One LDS-DMA piece (buffer_load_dwordx4 ... lds: 64 lanes x 16 B into LDS at dst + 16 * lane)
+// issued through inline asm.  With __builtin_amdgcn_raw_ptr_buffer_load_lds the compiler
+// sees an LDS write behind the load and puts s_waitcnt vmcnt(0) before the next LDS read, so
+// a next-tile prefetch issued before the current tile's MFMAs is waited for before those
+// MFMAs start (no overlap at all).  Kernels that use this order LDS themselves: counted
+// s_waitcnt vmcnt + barrier before reading what the DMA wrote.  (s_nop 0: the one wait state
+// an SALU write of M0 needs before an LDS-DMA reads it.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* dst, unsigned voff) {
+  typedef __attribute__((address_space(3))) void* lds_vp;
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_vp)(void*)dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(voff), "s"(r) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 }  // namespace dvie

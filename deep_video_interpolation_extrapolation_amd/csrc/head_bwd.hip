@@ -142,7 +142,7 @@ __global__ __launch_bounds__(512) void head3_bwd_kernel(const dvie_head3_bwd_des
       const int y = T.y0 + (P >> 6), x = T.x0 + (P & 63);
       const bool ok = y < p.hgt && x < p.wid;
       const unsigned o = ok ? (unsigned)((T.n * p.hgt + y) * p.wid + x) * hrow + (unsigned)(gq & 15) * 16u : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (lds_ptr_hb)(S + (wave + NW * q) * 1024), 16, o, 0, 0, 0);
+      lds_dma16(rh, S + (wave + NW * q) * 1024, o);
     }
 #pragma unroll
     for (int q = 0; q < C::GQ; ++q) {
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(512) void head3_bwd_kernel(const dvie_head3_bwd_des
       const int iy = T.y0 + p.dy0 + ((v >> 16) & 0xFF), ix = T.x0 + p.dx0 + ((v >> 4) & 0xFFF);
       const bool ok = v >= 0 && (unsigned)iy < (unsigned)p.hgt && (unsigned)ix < (unsigned)p.wid;
       const unsigned o = ok ? (unsigned)((T.n * p.hgt + iy) * p.wid + ix) * grow + (unsigned)(v & 15) * 16u : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_ptr_hb)(S + C::HT + pc * 1024), 16, o, 0, 0, 0);
+      lds_dma16(rg, S + C::HT + pc * 1024, o);
     }
   };
 

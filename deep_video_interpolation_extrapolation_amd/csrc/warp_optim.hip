@@ -100,14 +100,21 @@ __device__ __forceinline__ float warp_blend(float a, float b, float c, float d, 
 // Forward: a wave covers 256 consecutive pixels of one row, 4 per lane 64 apart: each gather
 // instruction reads the sources of 64 consecutive output pixels (a few cache lines for a
 // smooth flow), and the flow loads and output stores are 256-byte coalesced runs.
+//
+// xcd: workgroups are dealt to the 8 XCDs round-robin by index; with xcd set (and a grid that
+// is a multiple of 8) workgroup b takes the job slot (b % 8) * (grid / 8) + b / 8, so each XCD
+// walks a contiguous band of rows and the source rows two neighbouring output rows share are
+// gathered into one L2 instead of two.
 template <int CC, int LAUX = 0, int SAUX = 0>
-__global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p) {
+__global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p, int xcd) {
   const int segs = (p.w + 255) >> 8;
   const long long hw = (long long)p.h * p.w;
   const int waves = p.n * p.h * segs;  // < 2^31 (checked at launch)
   const int lane = threadIdx.x & 63;
+  const int g = gridDim.x;
+  const int vb = (xcd && (g & 7) == 0) ? (int)(blockIdx.x & 7) * (g >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   // wave-uniform row/segment (readfirstlane), so the plane buffer resources are scalar
-  for (int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6)); wv < waves;
+  for (int wv = __builtin_amdgcn_readfirstlane(vb * 4 + (threadIdx.x >> 6)); wv < waves;
        wv += gridDim.x * 4) {
     const int sg = wv % segs;
     const int r = wv / segs;
@@ -532,7 +539,8 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->out && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
   const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
   DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
-  int grid = grid_for(waves * 256);
+  // one workgroup per 4 waves (jobs) up to 8192 workgroups
+  int grid = (int)((waves + 3) / 4 < 8192 ? (waves + 3) / 4 : 8192);
   if (const char* e = getenv("DVIE_WARP_FWD_GRID")) {  // A/B: blocks = min(jobs / 4, cap)
     const long long need = (waves + 3) / 4, cap = atoi(e);
     if (cap > 0) grid = (int)(need < cap ? need : cap);
@@ -542,14 +550,19 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   // DVIE_WARP_NT (A/B, read per launch): 0 = default policy, 1 = non-temporal stores only
   const char* nt = getenv("DVIE_WARP_NT");
   const int ntm = nt && *nt ? atoi(nt) : 2;
+  // XCD bands pay off once the frames outgrow the L2s: 8x3x1024x2048 121.0 -> 100.2 us
+  // (0.555 -> 0.670 of HBM), while at 8x3x256x512 (12.6 MB) they cost 7.2 -> 8.6 us
+  // (profiles/r04aa/).  DVIE_WARP_XCD (A/B, read per launch): 1 = always, 0 = never
+  const char* xe = getenv("DVIE_WARP_XCD");
+  const int xcd = xe && *xe ? atoi(xe) : ((long long)d->n * d->c * d->h * d->w * 4 > (64ll << 20));
   if (d->c == 3 && ntm == 1)
-    hipLaunchKernelGGL((warp_fwd_kernel<3, 0, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL((warp_fwd_kernel<3, 0, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else if (d->c == 3 && ntm == 2)
-    hipLaunchKernelGGL((warp_fwd_kernel<3, 2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL((warp_fwd_kernel<3, 2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else if (d->c == 3)
-    hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else
-    hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d);
+    hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   DVIE_RETURN_LAUNCH();
 }
 

@@ -81,7 +81,11 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 // summed through LDS into one partial slab per split.  NW = 4 (output channels <= 32, the
 // 448 -> 3 / 448 -> 20 heads): no co half -- the second half's waves would only multiply the
 // zero padding of channels 32..63, and without them each wave has its SIMD's MFMA pipe alone.
-template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8>
+//
+// PIPE: the next k-step's fragments (its G fragment and all NT * TMI shifted X fragments) are
+// read from LDS while the current k-step's MFMAs run (two fragment sets in registers), instead
+// of each MFMA waiting on the transposed reads issued just before it.
+template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
                                                              int tiles_x, int tiles_y, int n_tiles, int flags) {
   typedef WgCfg<TH, TW, PR, TMO, TMI> C;
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
         const unsigned o = (oy < p.oh && ox < p.ow && c0 + ch < p.cout)
                                ? (unsigned)((T.n * p.oh + oy) * p.ow + ox) * grow + (unsigned)ch * 2u
                                : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_ptr_wg)(G + pc * 1024), 16, o, 0, 0, 0);
+        lds_dma16(rg, G + pc * 1024, o);
       }
     }
   };
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
       const bool ok = hx < 64 + TW - 1 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw && k0 + ch < p.c;
       const unsigned o = ok ? (unsigned)((T.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)ch * 2u : OOB;
       char* dst = smem + 2 * C::GSZ + sub * C::XSUB + (slot * C::XW + piece * 8) * 128;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_wg)dst, 16, o, 0, 0, 0);
+      lds_dma16(rx, dst, o);
     }
   };
 
@@ -230,6 +234,63 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
     }
     const char* G = smem + gb * C::GSZ;
     const char* X = smem + 2 * C::GSZ;
+    if constexpr (PIPE) {
+      constexpr int NS = (PR / 2) * 4, NB = C::NT * TMI;
+      const int ys = T.y0 % C::R;  // ring slot of the tile's first halo row
+      bf16x8 pa[2][TMO], pb[2][NB];
+      auto load = [&](int st, int k) {
+        const int py = wrow * (PR / 2) + (st >> 2), kx = st & 3;
+        const int gr = py * 64 + kx * 16;
+#pragma unroll
+        for (int j = 0; j < TMO; ++j) pa[k][j] = tr_pair(G + g_off[j] + gr * 128, G + g_off[j] + gr * 128 + 4 * 128);
+#pragma unroll
+        for (int ti = 0; ti < TH; ++ti) {
+          int slot = ys + py + ti;  // < 2R
+          slot -= slot >= C::R ? C::R : 0;
+          const char* Xr = X + slot * (C::XW * 128);
+#pragma unroll
+          for (int tj = 0; tj < TW; ++tj) {
+            const int xr = kx * 16 + tj;
+            const int m = xr & 3, xb = xr - m;
+#pragma unroll
+            for (int ji = 0; ji < TMI; ++ji)
+              pb[k][(ti * TW + tj) * TMI + ji] =
+                  tr_pair(Xr + x_off[m][ji] + xb * 128, Xr + x_off[m][ji] + xb * 128 + 4 * 128);
+          }
+        }
+      };
+      auto mma = [&](int k) {
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+          for (int ji = 0; ji < TMI; ++ji)
+#pragma unroll
+            for (int jo = 0; jo < TMO; ++jo) {
+              f32x16& c = acc[(t * TMO + jo) * TMI + ji];
+              const bf16x8 b = pb[k][t * TMI + ji];
+              if (dbg & 16)
+                c[0] += __builtin_bit_cast(float, __builtin_bit_cast(i32x4, pa[k][jo])[0] ^ __builtin_bit_cast(i32x4, b)[1]);
+              else
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[k][jo], b, c, 0, 0, 0);
+            }
+#pragma unroll
+        for (int j = 0; j < TMO; ++j) bsum[j] = sum8_bf16(pa[k][j], bsum[j]);
+      };
+      load(0, 0);
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        if (st + 1 < NS) load(st + 1, (st + 1) & 1);
+        mma(st & 1);
+        if (st + 1 < NS) {  // each MFMA followed by two of the next step's transposed reads
+#pragma unroll
+          for (int i = 0; i < NB * TMO; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the next step's reads stay in this step
+      }
+    } else
 #pragma unroll
     for (int pyl = 0; pyl < PR / 2; ++pyl)
 #pragma unroll
@@ -367,9 +428,8 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
       const int ch = 64 * sub + lcs * 8;
       const unsigned og = P < npix && c0 + ch < p.cout ? (unsigned)P * grow + (unsigned)ch * 2u : OOB;
       const unsigned ox = P < npix && k0 + ch < p.c ? (unsigned)P * xrow + (unsigned)ch * 2u : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_ptr_wg)(smem + buf * TSZ + sub * SUB + pr * 1024), 16, og, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_wg)(smem + (2 + buf) * TSZ + sub * SUB + pr * 1024), 16, ox,
-                                               0, 0, 0);
+      lds_dma16(rg, smem + buf * TSZ + sub * SUB + pr * 1024, og);
+      lds_dma16(rx, smem + (2 + buf) * TSZ + sub * SUB + pr * 1024, ox);
     }
   };
   const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
@@ -538,6 +598,12 @@ static int wg_dbg() {
 // kernels (A/B runs)
 static const int wg_setprio = getenv("DVIE_SETPRIO") && *getenv("DVIE_SETPRIO") == '1' ? 2 : 0;
 
+// DVIE_WG_PIPE (A/B, read per launch): 0 = 3x3 weight gradients without the fragment pipeline
+static bool wg_pipe_on() {
+  const char* e = getenv("DVIE_WG_PIPE");
+  return !(e && *e == '0');
+}
+
 // bias partial slabs the halo kernels write to p.bws (0: the launch is not theirs)
 int wgrad_halo_bias_slabs(const dvie_wgrad_desc& p) {
   if (!wgrad_halo_eligible(p)) return 0;
@@ -554,6 +620,7 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   int tiles_x, tiles_y, n_tiles, n_co, n_ci;
   wgrad_tiles(p, w, tiles_x, tiles_y, n_tiles, n_co, n_ci);
   const int grid = n_co * n_ci * p.splits;
+  const bool wg_pipe = wg_pipe_on();
   if (w.wide) {
     hipLaunchKernelGGL(wgrad_wide_kernel, dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, n_tiles);
     return true;
@@ -561,7 +628,10 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
   hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
                      tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio | wg_dbg())
-  if (p.th == 3 && p.cout <= 32 && !wg_narrow_env_off)
+  if (p.th == 3 && p.cout > 32 && wg_pipe)
+    hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
+                       tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio | wg_dbg());
+  else if (p.th == 3 && p.cout <= 32 && !wg_narrow_env_off)
     hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 4, 1, 1, 4>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   else if (p.th == 3)

@@ -18,6 +18,12 @@ pytestmark = pytest.mark.gpu
 
 CASES = [  # n, H, W, c, cout, k, stride, dtype
     (2, 37, 90, 64, 64, 3, 1, "bf16"),     # halo 3x3
+    # 3x3 halo kernel with several tiles per workgroup: ranges that cross column ends (ring
+    # refills), a ragged last column; a partial output-channel block; 128 channels (2 x 2
+    # channel blocks)
+    (8, 100, 200, 64, 64, 3, 1, "bf16"),
+    (4, 37, 300, 64, 96, 3, 1, "bf16"),
+    (2, 70, 130, 128, 128, 3, 1, "bf16"),
     (2, 40, 70, 448, 24, 3, 1, "bf16"),    # halo 3x3, narrow output (seg head)
     (1, 33, 65, 448, 8, 3, 1, "bf16"),     # halo 3x3, narrow output (rgb head), ragged tiles
     (2, 37, 77, 128, 128, 1, 1, "bf16"),   # halo 1x1
