@@ -18,6 +18,13 @@ import torch
 from . import _lib as L
 
 
+
+def _owner(p):
+    """the FlatParams module whose flat buffer holds parameter p (runtime.FlatParams keeps a
+    weak reference on the parameter), or None"""
+    r = getattr(p, "_dvie_owner", None)
+    return r() if r is not None else None
+
 class _FusedOptimizer(torch.optim.Optimizer):
     STATE = ("exp_avg", "exp_inf")
 
@@ -91,8 +98,8 @@ class _FusedOptimizer(torch.optim.Optimizer):
     def _flat_group(self, gi, group):
         """(owner, flat state 0, flat state 1) if the group maps onto one flat buffer."""
         ps = group["params"]
-        owner = getattr(ps[0], "_dvie_owner", None) if ps else None
-        if owner is None or any(getattr(p, "_dvie_owner", None) is not owner for p in ps):
+        owner = _owner(ps[0]) if ps else None
+        if owner is None or any(_owner(p) is not owner for p in ps):
             return None
         flat = owner._flat
         if sum(p.numel() for p in ps) != flat.numel():

@@ -51,7 +51,12 @@ class FlatParams:
             specs.append((off, n, tuple(p.shape)))
             off += n
         for p in params:
-            p._dvie_owner = self  # lets optim.Adamax take the one-launch flat path
+            # lets optim.Adamax take the one-launch flat path; a weak reference, so that the
+            # module -> plan -> layer -> parameter -> module loop holds no strong edge back to
+            # the module (torch does not traverse a tensor's __dict__ for the cycle collector
+            # while C++ also refers to the tensor: such a loop kept whole plans -- 100+ GB
+            # at 1024x2048 -- alive after their model was deleted)
+            p._dvie_owner = weakref.ref(self)
         self._flat_params = params
         self._flat_specs = specs
         self._flat = flat
