@@ -20,6 +20,8 @@
 // Reference op replaced: nn.Conv2d backward-weight (nets/HRNet.py, nets/vgg.py).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -129,16 +131,29 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
   const int lcs = lch ^ (((lrow >> 1) & 1) << 2);
 
   struct TilePos {
-    int n, y0, x0, col;
+    int n, y0, x0, col, ty, tx;
   };
-  auto tpos = [&](int t) {
+  auto tpos = [&](int t) {  // (divisions: once per workgroup)
     TilePos q;
-    const int ty = t % tiles_y;
-    const int r = t / tiles_y;
-    q.x0 = (r % tiles_x) * 64;
-    q.n = r / tiles_x;
-    q.y0 = ty * PR;
-    q.col = r;
+    q.ty = t % tiles_y;
+    q.col = t / tiles_y;
+    q.tx = q.col % tiles_x;
+    q.n = q.col / tiles_x;
+    q.x0 = q.tx * 64;
+    q.y0 = q.ty * PR;
+    return q;
+  };
+  auto tnext = [&](TilePos q) {  // tile t + 1 from tile t (scalar increments, no divisions)
+    if (++q.ty == tiles_y) {
+      q.ty = 0;
+      ++q.col;
+      if (++q.tx == tiles_x) {
+        q.tx = 0;
+        ++q.n;
+      }
+    }
+    q.x0 = q.tx * 64;
+    q.y0 = q.ty * PR;
     return q;
   };
 
@@ -160,9 +175,10 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
       }
     }
   };
-  // halo rows [h0, h1) (relative to tile T's first halo row) into their ring slots
-  auto issue_x = [&](const TilePos& T, int h0, int h1) {
-    const int npc = (h1 - h0) * C::XPR;  // pieces per sub-image
+  // halo rows [h0, h0 + NR) (relative to tile T's first halo row) into their ring slots
+  // (nr: std::integral_constant<int, NR>, so the piece -> row divisions are by constants)
+  auto issue_x = [&](const TilePos& T, int h0, auto nr) {
+    constexpr int npc = decltype(nr)::value * C::XPR;  // pieces per sub-image
 #pragma unroll 1
     for (int pc = wave; pc < TMI * npc; pc += NW) {
       const int sub = pc / npc, rem = pc - sub * npc;
@@ -218,19 +234,21 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
   if (t_begin < t_end) {
     const TilePos T0 = tpos(t_begin);
     issue_g(T0, 0);
-    issue_x(T0, 0, C::HR);
+    issue_x(T0, 0, std::integral_constant<int, C::HR>());
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
   int gb = 0;
+  TilePos Tc = tpos(t_begin < t_end ? t_begin : 0);
   for (int tile = t_begin; tile < t_end; ++tile, gb ^= 1) {
-    const TilePos T = tpos(tile);
+    const TilePos T = Tc;
     const bool has_next = tile + 1 < t_end;
-    const TilePos TN = tpos(has_next ? tile + 1 : tile);
+    const TilePos TN = has_next ? tnext(T) : T;
+    Tc = TN;
     const bool same_col = has_next && TN.col == T.col;
     if (same_col && !(dbg & 8)) {  // next tile: its G tile and its PR new halo rows
       issue_g(TN, gb ^ 1);
-      issue_x(TN, C::HR - PR, C::HR);
+      issue_x(TN, C::HR - PR, std::integral_constant<int, PR>());
     }
     const char* G = smem + gb * C::GSZ;
     const char* X = smem + 2 * C::GSZ;
@@ -332,7 +350,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
     __syncthreads();
     if (has_next && !same_col) {  // column change: refill the whole ring (pipeline restart)
       issue_g(TN, gb ^ 1);
-      issue_x(TN, 0, C::HR);
+      issue_x(TN, 0, std::integral_constant<int, C::HR>());
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
