@@ -231,7 +231,7 @@ EXPORTS = [
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
     "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs", "dvie_head3_bwd",
-    "dvie_segenc_fwd", "dvie_segenc_bwd",
+    "dvie_segenc_fwd", "dvie_segenc_bwd", "dvie_pack_blocks", "dvie_trace_kernels", "dvie_traced_kernels",
 ]
 
 _lib = None
@@ -270,7 +270,11 @@ def load():
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]
-        for name in ("dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_bn_partial_splits"):
+        lib.dvie_trace_kernels.argtypes = [i32]
+        lib.dvie_trace_kernels.restype = i32
+        lib.dvie_traced_kernels.argtypes = []
+        lib.dvie_traced_kernels.restype = ctypes.c_char_p
+        for name in ("dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_bn_partial_splits", "dvie_pack_blocks"):
             getattr(lib, name).argtypes = [vp]
             getattr(lib, name).restype = i32
         lib.dvie_run_ops.argtypes = [vp, i32, vp]

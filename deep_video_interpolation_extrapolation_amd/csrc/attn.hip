@@ -826,31 +826,31 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
       if ((d->op == DVIE_ATTN_GATHER || d->op == DVIE_ATTN_GATHER_T) && tiled && bf && d->c % 32 == 0 &&
           d->b_ld % 8 == 0 && gm_on()) {
         if (d->op == DVIE_ATTN_GATHER)
-          hipLaunchKernelGGL(attn_gather_mfma_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_gather_mfma_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         else
-          hipLaunchKernelGGL(attn_gather_mfma_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_gather_mfma_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         break;
       }
       if (tiled && d->op == DVIE_ATTN_GATHER) {
         if (bf)
-          hipLaunchKernelGGL(attn_gather_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_gather_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         else
-          hipLaunchKernelGGL(attn_gather_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_gather_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         break;
       }
       if (tiled && d->op == DVIE_ATTN_GATHER_T) {
         if (bf)
-          hipLaunchKernelGGL(attn_gather_t_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_gather_t_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         else
-          hipLaunchKernelGGL(attn_gather_t_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_gather_t_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         break;
       }
       const long long tot = npx * (d->c / 4);
       const dim3 grid((unsigned)((tot + 255) / 256));
       if (bf)
-        hipLaunchKernelGGL(attn_vec_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_vec_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
       else
-        hipLaunchKernelGGL(attn_vec_kernel<float>, grid, dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_vec_kernel<float>, grid, dim3(256), 0, s, *d);
       break;
     }
     case DVIE_ATTN_CORR: {
@@ -858,22 +858,22 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
       DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0, "attn: corr c=%d", d->c);
       DVIE_CHECK_ARG(d->y_ld >= d->nhalf * K, "attn: corr y_ld");
       if (tiled && bf && d->c % 32 == 0 && d->a_ld % 8 == 0 && d->b_ld % 8 == 0 && gm_on()) {
-        hipLaunchKernelGGL(attn_corr_mfma_kernel, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_corr_mfma_kernel, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         break;
       }
       if (tiled) {
         if (bf)
-          hipLaunchKernelGGL(attn_corr_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_corr_tile_kernel<bf16_t>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         else
-          hipLaunchKernelGGL(attn_corr_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+          DVIE_LAUNCH(attn_corr_tile_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         break;
       }
       const long long tot = npx * d->nhalf * K;
       const dim3 grid((unsigned)((tot + 255) / 256));
       if (bf)
-        hipLaunchKernelGGL(attn_corr_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_corr_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
       else
-        hipLaunchKernelGGL(attn_corr_kernel<float>, grid, dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_corr_kernel<float>, grid, dim3(256), 0, s, *d);
       break;
     }
     default: {
@@ -887,9 +887,9 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
         DVIE_CHECK_ARG(d->nhalf == 1 || d->nhalf == 2, "attn: wnorm takes one or two maps");
       const dim3 grid((unsigned)((npx + (256 / RG) - 1) / (256 / RG)));
       if (bf)
-        hipLaunchKernelGGL(attn_row_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_row_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
       else
-        hipLaunchKernelGGL(attn_row_kernel<float>, grid, dim3(256), 0, s, *d);
+        DVIE_LAUNCH(attn_row_kernel<float>, grid, dim3(256), 0, s, *d);
     }
   }
   DVIE_RETURN_LAUNCH();

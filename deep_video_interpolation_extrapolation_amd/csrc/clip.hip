@@ -81,9 +81,9 @@ int dvie_clip_prep(const dvie_clip_desc* d, void* stream) {
   long long blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   if (v4)
-    hipLaunchKernelGGL(clip_prep_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *d);
+    DVIE_LAUNCH(clip_prep_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *d);
   else
-    hipLaunchKernelGGL(clip_prep_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *d);
+    DVIE_LAUNCH(clip_prep_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
 

@@ -35,6 +35,17 @@ void set_error(const char* fmt, ...);
 #define DVIE_DBG(x) 0
 #endif
 
+// Launch trace (diagnostics: dvie_trace_kernels / dvie_traced_kernels in include/dvie.h).
+// Every kernel launch of the library goes through DVIE_LAUNCH, which notes the kernel's host
+// stub when the calling thread has tracing on (one thread-local flag test otherwise).
+extern thread_local bool g_trace_on;
+void trace_launch(const void* fn);
+#define DVIE_LAUNCH(kern, ...)                                                       \
+  do {                                                                               \
+    if (::dvie::g_trace_on) ::dvie::trace_launch(reinterpret_cast<const void*>(kern)); \
+    hipLaunchKernelGGL(kern, __VA_ARGS__);                                           \
+  } while (0)
+
 #define DVIE_RETURN_LAUNCH()                     \
   do {                                           \
     hipError_t _e = hipGetLastError();           \

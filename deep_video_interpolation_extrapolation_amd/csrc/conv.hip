@@ -9,9 +9,15 @@
 //
 // Reference ops replaced: nn.Conv2d forward / backward of nets/HRNet.py (all 77 convs)
 // and nets/vgg.py:11-54 (VGG19 features).
+#include <cxxabi.h>
+#include <dlfcn.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <string>
+#include <vector>
 
 #include "common.h"
 
@@ -25,6 +31,30 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 const char* last_error() { return g_err; }
+
+// launch trace (dvie_trace_kernels): the host stubs of the kernels this thread launched
+thread_local bool g_trace_on = false;
+static thread_local std::vector<const void*> g_trace;
+static thread_local std::string g_trace_text;
+void trace_launch(const void* fn) {
+  if (g_trace.size() < 4096) g_trace.push_back(fn);
+}
+
+static std::string kernel_name(const void* fn) {
+  const char* m = hipKernelNameRefByPtr(fn, nullptr);
+  Dl_info info;
+  if (!m && dladdr(fn, &info) && info.dli_sname) m = info.dli_sname;
+  if (!m) {
+    char b[32];
+    snprintf(b, sizeof(b), "%p", fn);
+    return b;
+  }
+  int st = 0;
+  char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+  std::string out = (st == 0 && d) ? d : m;
+  free(d);
+  return out;
+}
 
 // ----------------------------------------------------------------------------------
 // weight gradient
@@ -526,9 +556,9 @@ static void launch_bias_colsum(const dvie_wgrad_desc& d, hipStream_t s) {
   c.dtype = d.dtype;
   const long long chunk = (c.rows + c.splits - 1) / c.splits;
   if (d.dtype == DVIE_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(c.splits), dim3(256), 0, s, c, chunk);
+    DVIE_LAUNCH(colsum_kernel<bf16_t>, dim3(c.splits), dim3(256), 0, s, c, chunk);
   else
-    hipLaunchKernelGGL(colsum_kernel<float>, dim3(c.splits), dim3(256), 0, s, c, chunk);
+    DVIE_LAUNCH(colsum_kernel<float>, dim3(c.splits), dim3(256), 0, s, c, chunk);
 }
 
 int dvie_wgrad_bias_slabs(const dvie_wgrad_desc* d) {
@@ -552,9 +582,9 @@ int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   if (d->bws) DVIE_CHECK_ARG(d->cout % 4 == 0 && d->cout <= 4096 && d->g_ld % 4 == 0, "wgrad: bias partials (cout=%d)", d->cout);
   if (wgrad_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();  // (bias sums fused when bws is set)
   if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, *d, chunk);
+    DVIE_LAUNCH(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, *d, chunk);
   else
-    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, s, *d, chunk);
+    DVIE_LAUNCH(wgrad_kernel<float>, grid, dim3(256), 0, s, *d, chunk);
   if (d->bws) launch_bias_colsum(*d, s);
   DVIE_RETURN_LAUNCH();
 }
@@ -568,10 +598,10 @@ int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream) {
   const long long total4 = (long long)(d->ws_rows - d->co_off) * d->ws_k / 4;
   if (total4 < 1) return DVIE_OK;
   if (total4 < 2048 && d->splits >= 256)
-    hipLaunchKernelGGL((wreduce_kernel<4, 64>), dim3((unsigned)((total4 + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+    DVIE_LAUNCH((wreduce_kernel<4, 64>), dim3((unsigned)((total4 + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                        *d);
   else
-    hipLaunchKernelGGL((wreduce_kernel<32, 8>), dim3((unsigned)((total4 + 31) / 32)), dim3(256), 0,
+    DVIE_LAUNCH((wreduce_kernel<32, 8>), dim3((unsigned)((total4 + 31) / 32)), dim3(256), 0,
                        (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
@@ -582,18 +612,44 @@ int dvie_colsum(const dvie_colsum_desc* d, void* stream) {
   const long long chunk = (d->rows + d->splits - 1) / d->splits;
   hipStream_t s = (hipStream_t)stream;
   if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(d->splits), dim3(256), 0, s, *d, chunk);
+    DVIE_LAUNCH(colsum_kernel<bf16_t>, dim3(d->splits), dim3(256), 0, s, *d, chunk);
   else
-    hipLaunchKernelGGL(colsum_kernel<float>, dim3(d->splits), dim3(256), 0, s, *d, chunk);
+    DVIE_LAUNCH(colsum_kernel<float>, dim3(d->splits), dim3(256), 0, s, *d, chunk);
   DVIE_RETURN_LAUNCH();
 }
 
 int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int blocks, void* stream) {
   DVIE_CHECK_ARG(descs_dev && n > 0 && blocks > 0, "pack: args (n %d, blocks %d)", n, blocks);
-  hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, descs_dev, n);
+  DVIE_LAUNCH(pack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, descs_dev, n);
   DVIE_RETURN_LAUNCH();
 }
 
 const char* dvie_last_error(void) { return dvie::last_error(); }
+
+int dvie_pack_blocks(const dvie_pack_desc* d) {
+  if (!d || d->rows <= 0 || d->kpad <= 0) return 0;
+  switch (pack_kind(*d)) {
+    case PACK_ROW: return d->rows;
+    case PACK_TILE: return cdiv(d->rows, PACK_TR) * cdiv(d->c, PACK_TC);
+    default: return cdiv((long long)d->rows * d->kpad, 1024);
+  }
+}
+
+int dvie_trace_kernels(int on) {
+  const int was = dvie::g_trace_on ? 1 : 0;
+  dvie::g_trace_on = on != 0;
+  dvie::g_trace.clear();
+  return was;
+}
+
+const char* dvie_traced_kernels(void) {
+  dvie::g_trace_text.clear();
+  for (size_t i = 0; i < dvie::g_trace.size(); ++i) {
+    if (i) dvie::g_trace_text += ';';
+    dvie::g_trace_text += dvie::kernel_name(dvie::g_trace[i]);
+  }
+  dvie::g_trace.clear();
+  return dvie::g_trace_text.c_str();
+}
 
 }  // extern "C"

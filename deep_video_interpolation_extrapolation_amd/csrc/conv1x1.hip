@@ -636,7 +636,7 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   const int n_ct = (p.cout + C::BC - 1) / C::BC;
   const int n_tiles = n_ct * ((npix + C::BP - 1) / C::BP);
   if (p.out_f32) {
-    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, true>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles, dbg_env());
+    DVIE_LAUNCH((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, true>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles, dbg_env());
     return;
   }
   if constexpr (NS >= 2 && NS <= 5 && MI * TMC <= 4) {
@@ -646,7 +646,7 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
     const int per_cu = 163840 / C::SMEM;
     const int G = 256 * (per_cu > 2 ? 2 : per_cu);
     if (persist_env_on() && p.c > KC && n_tiles > G) {
-      hipLaunchKernelGGL((conv1x1_persist_kernel<TMC, NS, KC, NWP, MI, NWC>), dim3(G), dim3(64 * NW), 0, s, p, n_ct,
+      DVIE_LAUNCH((conv1x1_persist_kernel<TMC, NS, KC, NWP, MI, NWC>), dim3(G), dim3(64 * NW), 0, s, p, n_ct,
                          n_tiles);
       return;
     }
@@ -665,7 +665,7 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
       switch (pre) {
 #define DVIE_1X1_CE_CASE(V)                                                                                          \
   case V:                                                                                                            \
-    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false, PreOk<V, NS, MI * TMC>::v, true>), dim3(n_tiles), \
+    DVIE_LAUNCH((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false, PreOk<V, NS, MI * TMC>::v, true>), dim3(n_tiles), \
                        dim3(64 * NW), 0, s, p, n_ct, n_tiles, 0);                                                     \
     return;
         DVIE_1X1_CE_CASE(0) DVIE_1X1_CE_CASE(1) DVIE_1X1_CE_CASE(2) DVIE_1X1_CE_CASE(3) DVIE_1X1_CE_CASE(4)
@@ -677,14 +677,14 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   switch (pre) {
 #define DVIE_1X1_PRE_CASE(V)                                                                                      \
   case V:                                                                                                        \
-    hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false, PreOk<V, NS, MI * TMC>::v>), dim3(n_tiles), \
+    DVIE_LAUNCH((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false, PreOk<V, NS, MI * TMC>::v>), dim3(n_tiles), \
                        dim3(64 * NW), 0, s, p, n_ct, n_tiles, dbg_env());                                                   \
     break;
     DVIE_1X1_PRE_CASE(1) DVIE_1X1_PRE_CASE(2) DVIE_1X1_PRE_CASE(3) DVIE_1X1_PRE_CASE(4) DVIE_1X1_PRE_CASE(5)
     DVIE_1X1_PRE_CASE(6) DVIE_1X1_PRE_CASE(7)
 #undef DVIE_1X1_PRE_CASE
     default:
-      hipLaunchKernelGGL((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles, dbg_env());
+      DVIE_LAUNCH((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, false>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles, dbg_env());
   }
 }
 

@@ -338,9 +338,9 @@ static void launch_conv(const dvie_conv_desc& p, hipStream_t s) {
   const int n_ct = (p.cout + BC - 1) / BC;
   const int n_tiles = (int)((npix + BP - 1) / BP) * n_ct;
   if (p.out_f32)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, BC, BP, WC, WP, true>), dim3(n_tiles), dim3(256), 0, s, p, n_ct, n_tiles);
+    DVIE_LAUNCH((conv_igemm_kernel<T, BC, BP, WC, WP, true>), dim3(n_tiles), dim3(256), 0, s, p, n_ct, n_tiles);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<T, BC, BP, WC, WP, false>), dim3(n_tiles), dim3(256), 0, s, p, n_ct,
+    DVIE_LAUNCH((conv_igemm_kernel<T, BC, BP, WC, WP, false>), dim3(n_tiles), dim3(256), 0, s, p, n_ct,
                        n_tiles);
 }
 

@@ -535,10 +535,10 @@ static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
     const int persistent = n_tiles > cap ? 1 : 0;
     const int grid = persistent ? cap : n_tiles;
     if (p.out_f32)
-      hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
+      DVIE_LAUNCH((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
                          n_tiles, tiles_x, tiles_y, persistent, halo_setprio | halo_wait_flag());
     else
-      hipLaunchKernelGGL((conv_halo_kernel<TM, WC, WP, TH, TW, false>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
+      DVIE_LAUNCH((conv_halo_kernel<TM, WC, WP, TH, TW, false>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
                          n_tiles, tiles_x, tiles_y, persistent, (epi_prefetch_on ? 1 : 0) | halo_setprio | halo_wait_flag());
     return true;
   }
@@ -815,10 +815,10 @@ static void launch_ws_rows(const dvie_conv_desc& p, hipStream_t s) {
   const int persistent = n_tiles > cap ? 1 : 0;
   const int grid = persistent ? cap : n_tiles;
   if (p.out_f32)
-    hipLaunchKernelGGL((conv_ws_kernel<KS, true, WP>), dim3(grid), dim3(2 * WP * 64), 0, s, p, n_tiles, tiles_x,
+    DVIE_LAUNCH((conv_ws_kernel<KS, true, WP>), dim3(grid), dim3(2 * WP * 64), 0, s, p, n_tiles, tiles_x,
                        tiles_y, persistent);
   else
-    hipLaunchKernelGGL((conv_ws_kernel<KS, false, WP>), dim3(grid), dim3(2 * WP * 64), 0, s, p, n_tiles, tiles_x,
+    DVIE_LAUNCH((conv_ws_kernel<KS, false, WP>), dim3(grid), dim3(2 * WP * 64), 0, s, p, n_tiles, tiles_x,
                        tiles_y, persistent);
 }
 
@@ -1084,7 +1084,7 @@ static void launch_strip_k(const dvie_conv_desc& p, hipStream_t s) {
   seg = (seg + WR - 1) / WR * WR;
   nseg = (p.oh + seg - 1) / seg;
   const int n_wg = cols * nseg;
-  hipLaunchKernelGGL((conv_strip_kernel<KS, EPI, WR, D>), dim3(n_wg), dim3(2 * WR * 64), 0, s, p, tiles_x, nseg, seg,
+  DVIE_LAUNCH((conv_strip_kernel<KS, EPI, WR, D>), dim3(n_wg), dim3(2 * WR * 64), 0, s, p, tiles_x, nseg, seg,
                      n_wg);
 }
 
@@ -1279,9 +1279,9 @@ static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
   if (per_cb > n_tiles) per_cb = n_tiles;
   const int grid = per_cb * n_cb;
   if (p.out_f32)
-    hipLaunchKernelGGL((conv_nk_kernel<CP8, true>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
+    DVIE_LAUNCH((conv_nk_kernel<CP8, true>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
   else
-    hipLaunchKernelGGL((conv_nk_kernel<CP8, false>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
+    DVIE_LAUNCH((conv_nk_kernel<CP8, false>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1634,7 +1634,7 @@ static bool h8_on() {
 template <int EPI>
 static void launch_h8(const dvie_conv_desc& p, hipStream_t s, int n_ct, int n_tiles, int tiles_x, int tiles_y) {
   const int grid = n_tiles > 256 ? 256 : n_tiles;
-  hipLaunchKernelGGL((conv_h8_kernel<EPI>), dim3(grid), dim3(H8::NTH), 0, s, p, n_ct, n_tiles, tiles_x, tiles_y);
+  DVIE_LAUNCH((conv_h8_kernel<EPI>), dim3(grid), dim3(H8::NTH), 0, s, p, n_ct, n_tiles, tiles_x, tiles_y);
 }
 
 // 3x3 stride-1 conv, identity taps (t3), bf16 output; true when the eight-row kernel took it

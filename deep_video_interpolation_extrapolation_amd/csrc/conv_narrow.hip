@@ -328,9 +328,9 @@ bool conv_narrow_launch(const dvie_conv_desc& p, hipStream_t s) {
   const int n_tiles = (int)nt;
   const int grid = n_tiles < 256 ? n_tiles : 256;  // one 150-KB workgroup per CU
   if (p.out_f32)
-    hipLaunchKernelGGL(conv_narrow_kernel<true>, dim3(grid), dim3(512), 0, s, p, tiles_x, tiles_y, n_tiles, narrow_dbg());
+    DVIE_LAUNCH(conv_narrow_kernel<true>, dim3(grid), dim3(512), 0, s, p, tiles_x, tiles_y, n_tiles, narrow_dbg());
   else
-    hipLaunchKernelGGL(conv_narrow_kernel<false>, dim3(grid), dim3(512), 0, s, p, tiles_x, tiles_y, n_tiles, narrow_dbg());
+    DVIE_LAUNCH(conv_narrow_kernel<false>, dim3(grid), dim3(512), 0, s, p, tiles_x, tiles_y, n_tiles, narrow_dbg());
   return true;
 }
 

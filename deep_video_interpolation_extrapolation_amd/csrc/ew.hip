@@ -451,18 +451,18 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
                       (d->nsrc < 3 || (d->sw2 <= d->w && d->sh2 <= d->h));
       if (d->op == DVIE_EW_FUSE && up && fuse2_on()) {
         const dim3 g2((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * d->h));
-        hipLaunchKernelGGL((ew_fuse2_kernel<bf16_t, 8>), g2, dim3(256), 0, s, *d, cq);
+        DVIE_LAUNCH((ew_fuse2_kernel<bf16_t, 8>), g2, dim3(256), 0, s, *d, cq);
       } else if (d->op == DVIE_EW_FUSE)
-        hipLaunchKernelGGL((ew_kernel<bf16_t, 8, DVIE_EW_FUSE>), grid, dim3(256), 0, s, *d, cq);
+        DVIE_LAUNCH((ew_kernel<bf16_t, 8, DVIE_EW_FUSE>), grid, dim3(256), 0, s, *d, cq);
       else if (d->op == DVIE_EW_UPT)
-        hipLaunchKernelGGL((ew_kernel<bf16_t, 8, DVIE_EW_UPT>), grid, dim3(256), 0, s, *d, cq);
+        DVIE_LAUNCH((ew_kernel<bf16_t, 8, DVIE_EW_UPT>), grid, dim3(256), 0, s, *d, cq);
       else
-        hipLaunchKernelGGL((ew_kernel<bf16_t, 8, -2>), grid, dim3(256), 0, s, *d, cq);
+        DVIE_LAUNCH((ew_kernel<bf16_t, 8, -2>), grid, dim3(256), 0, s, *d, cq);
     } else {
-      hipLaunchKernelGGL((ew_kernel<bf16_t, 4, -1>), grid, dim3(256), 0, s, *d, cq);
+      DVIE_LAUNCH((ew_kernel<bf16_t, 4, -1>), grid, dim3(256), 0, s, *d, cq);
     }
   } else {
-    hipLaunchKernelGGL((ew_kernel<float, 4, -1>), grid, dim3(256), 0, s, *d, cq);
+    DVIE_LAUNCH((ew_kernel<float, 4, -1>), grid, dim3(256), 0, s, *d, cq);
   }
   DVIE_RETURN_LAUNCH();
 }

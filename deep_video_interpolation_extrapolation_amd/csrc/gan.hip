@@ -324,16 +324,16 @@ static void bn_launch(const dvie_bn_desc* d, hipStream_t st, int bwd) {
   const long long rps = (d->rows + d->splits - 1) / d->splits;
   if (!bwd) {
     if (d->training)
-      hipLaunchKernelGGL((bn_stats_kernel<TX, TX>), dim3(d->splits), dim3(BN_THREADS), 0, st, (const TX*)d->x,
+      DVIE_LAUNCH((bn_stats_kernel<TX, TX>), dim3(d->splits), dim3(BN_THREADS), 0, st, (const TX*)d->x,
                          d->x_ld, (const TX*)nullptr, 0LL, (const float*)nullptr, d->rows, d->c, rps, d->partial, 0);
-    hipLaunchKernelGGL(bn_fold_fwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
+    DVIE_LAUNCH(bn_fold_fwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
   } else {
-    hipLaunchKernelGGL((bn_stats_kernel<T, TX>), dim3(d->splits), dim3(BN_THREADS), 0, st, (const T*)d->g, d->g_ld,
+    DVIE_LAUNCH((bn_stats_kernel<T, TX>), dim3(d->splits), dim3(BN_THREADS), 0, st, (const T*)d->g, d->g_ld,
                        (const TX*)d->x, d->x_ld, (const float*)d->stats, d->rows, d->c, rps, d->partial, 1);
-    hipLaunchKernelGGL(bn_fold_bwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
+    DVIE_LAUNCH(bn_fold_bwd_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, *d);
   }
   const long long n4 = d->rows * (d->c / 4);
-  hipLaunchKernelGGL((bn_apply_kernel<TX, T>), dim3(grid_1d(n4)), dim3(256), 0, st, *d, bwd);
+  DVIE_LAUNCH((bn_apply_kernel<TX, T>), dim3(grid_1d(n4)), dim3(256), 0, st, *d, bwd);
 }
 
 static void bn_dispatch(const dvie_bn_desc* d, hipStream_t st, int bwd) {
@@ -389,10 +389,10 @@ int dvie_head_fwd(const dvie_head_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const long long np = (long long)d->n * (d->h / d->pool) * (d->w / d->pool);
   if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(head_pool_kernel<bf16_t>, dim3(grid_1d(np * d->c)), dim3(256), 0, st, *d);
+    DVIE_LAUNCH(head_pool_kernel<bf16_t>, dim3(grid_1d(np * d->c)), dim3(256), 0, st, *d);
   else
-    hipLaunchKernelGGL(head_pool_kernel<float>, dim3(grid_1d(np * d->c)), dim3(256), 0, st, *d);
-  hipLaunchKernelGGL(head_mean_kernel, dim3(grid_1d(np)), dim3(256), 0, st, *d);
+    DVIE_LAUNCH(head_pool_kernel<float>, dim3(grid_1d(np * d->c)), dim3(256), 0, st, *d);
+  DVIE_LAUNCH(head_mean_kernel, dim3(grid_1d(np)), dim3(256), 0, st, *d);
   DVIE_RETURN_LAUNCH();
 }
 
@@ -401,22 +401,22 @@ int dvie_head_bwd(const dvie_head_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const long long n4 = (long long)d->n * d->h * d->w * (d->c / 4);
   if (d->dtype == DVIE_BF16)
-    hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(grid_1d(n4)), dim3(256), 0, st, *d);
+    DVIE_LAUNCH(head_bwd_kernel<bf16_t>, dim3(grid_1d(n4)), dim3(256), 0, st, *d);
   else
-    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(grid_1d(n4)), dim3(256), 0, st, *d);
+    DVIE_LAUNCH(head_bwd_kernel<float>, dim3(grid_1d(n4)), dim3(256), 0, st, *d);
   DVIE_RETURN_LAUNCH();
 }
 
 int dvie_softmax_fwd(const dvie_softmax_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->x && d->y && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "softmax fwd: args");
-  hipLaunchKernelGGL(softmax_fwd_kernel, dim3(grid_1d((long long)d->n * d->h * d->w)), dim3(256), 0,
+  DVIE_LAUNCH(softmax_fwd_kernel, dim3(grid_1d((long long)d->n * d->h * d->w)), dim3(256), 0,
                      (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
 
 int dvie_softmax_bwd(const dvie_softmax_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->y && d->gy && d->gx && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "softmax bwd: args");
-  hipLaunchKernelGGL(softmax_bwd_kernel, dim3(grid_1d((long long)d->n * d->h * d->w)), dim3(256), 0,
+  DVIE_LAUNCH(softmax_bwd_kernel, dim3(grid_1d((long long)d->n * d->h * d->w)), dim3(256), 0,
                      (hipStream_t)stream, *d);
   DVIE_RETURN_LAUNCH();
 }
@@ -425,7 +425,7 @@ int dvie_adam(float* p, const float* g, float* m, float* v, long long n, float s
               float eps, float wd, void* stream) {
   DVIE_CHECK_ARG(p && g && m && v && n >= 0, "adam: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, step_size, b1,
+  DVIE_LAUNCH(adam_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, step_size, b1,
                      b2, eps, wd, (const float*)nullptr, 0.0, 0.0, 0.0);
   DVIE_RETURN_LAUNCH();
 }
@@ -434,7 +434,7 @@ int dvie_adam_dev(float* p, const float* g, float* m, float* v, long long n, dou
                   double eps, double wd, const float* step, void* stream) {
   DVIE_CHECK_ARG(p && g && m && v && step && n >= 0, "adam_dev: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, 0.f,
+  DVIE_LAUNCH(adam_kernel, dim3(grid_1d(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, 0.f,
                      (float)b1, (float)b2, (float)eps, (float)wd, step, lr, b1, b2);
   DVIE_RETURN_LAUNCH();
 }

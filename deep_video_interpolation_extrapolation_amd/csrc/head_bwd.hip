@@ -312,8 +312,8 @@ extern "C" int dvie_head3_bwd(const dvie_head3_bwd_desc* d, void* stream) {
   const int grid = n_cb * d->splits;
   hipStream_t s = (hipStream_t)stream;
   if (d->cout == 8)
-    hipLaunchKernelGGL(head3_bwd_kernel<8>, dim3(grid), dim3(512), 0, s, *d, n_cb, tiles_x, tiles_y, (int)nt);
+    DVIE_LAUNCH(head3_bwd_kernel<8>, dim3(grid), dim3(512), 0, s, *d, n_cb, tiles_x, tiles_y, (int)nt);
   else
-    hipLaunchKernelGGL(head3_bwd_kernel<24>, dim3(grid), dim3(512), 0, s, *d, n_cb, tiles_x, tiles_y, (int)nt);
+    DVIE_LAUNCH(head3_bwd_kernel<24>, dim3(grid), dim3(512), 0, s, *d, n_cb, tiles_x, tiles_y, (int)nt);
   DVIE_RETURN_LAUNCH();
 }

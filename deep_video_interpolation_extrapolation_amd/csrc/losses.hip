@@ -532,44 +532,44 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
   switch (d->kind) {
     case DVIE_LOSS_L1:
     case DVIE_LOSS_GDL:
-      hipLaunchKernelGGL(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, 0);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
+      DVIE_LAUNCH(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, 0);
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
                          d->kind == DVIE_LOSS_L1 ? 1.0 / tot : 1.0, 0.0, vs, acc);
       break;
     case DVIE_LOSS_MSE:
-      hipLaunchKernelGGL(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, lp.per_sample);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.per_sample, d->bsz, d->out,
+      DVIE_LAUNCH(l1gdl_kernel, lp.grid, dim3(RB), 0, s, *d, lp.per_sample);
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.per_sample, d->bsz, d->out,
                          1.0 / ((double)d->ch * d->h * d->w), 0.0, vs, acc);
       break;
     case DVIE_LOSS_CE:
-      hipLaunchKernelGGL(ce_kernel, lp.grid, dim3(RB), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0, vs, acc);
+      DVIE_LAUNCH(ce_kernel, lp.grid, dim3(RB), 0, s, *d);
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0, vs, acc);
       break;
     case DVIE_LOSS_SSIM:
-      hipLaunchKernelGGL(ssim_fwd_kernel, lp.grid, dim3(256), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, -1.0 / tot,
+      DVIE_LAUNCH(ssim_fwd_kernel, lp.grid, dim3(256), 0, s, *d);
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, -1.0 / tot,
                          1.0, vs, acc);
-      if (d->grad) hipLaunchKernelGGL(ssim_bwd_kernel, lp.grid, dim3(256), 0, s, *d);
+      if (d->grad) DVIE_LAUNCH(ssim_bwd_kernel, lp.grid, dim3(256), 0, s, *d);
       break;
     case DVIE_LOSS_L1NHWC:
       if (d->dtype == DVIE_BF16)
-        hipLaunchKernelGGL(l1nhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d);
+        DVIE_LAUNCH(l1nhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d);
       else
-        hipLaunchKernelGGL(l1nhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / tot, 0.0, vs, acc);
+        DVIE_LAUNCH(l1nhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d);
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / tot, 0.0, vs, acc);
       break;
     case DVIE_LOSS_COSNHWC:
       if (d->dtype == DVIE_BF16)
-        hipLaunchKernelGGL(cosnhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
+        DVIE_LAUNCH(cosnhwc_kernel<bf16_t>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
       else
-        hipLaunchKernelGGL(cosnhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
+        DVIE_LAUNCH(cosnhwc_kernel<float>, lp.grid, dim3(RB), 0, s, *d, cos_lanes(d->ch));
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out,
                          (double)d->weight / px, 0.0, vs, acc);
       break;
     case DVIE_LOSS_IOU:
     case DVIE_LOSS_ARGMAX_IOU:
-      hipLaunchKernelGGL(iou_kernel, lp.grid, dim3(RB), 0, s, *d);
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0, vs, acc);
+      DVIE_LAUNCH(iou_kernel, lp.grid, dim3(RB), 0, s, *d);
+      DVIE_LAUNCH(finalize_kernel, dim3(1), dim3(RB), 0, s, d->partial, lp.blocks, 1, d->out, 1.0 / px, 0.0, vs, acc);
       break;
     default:
       DVIE_CHECK_ARG(false, "loss: unknown kind %d", d->kind);
@@ -579,7 +579,7 @@ int dvie_loss(const dvie_loss_desc* d, void* stream) {
 
 int dvie_sum_f32(const float* x, int n, float* out, void* stream) {
   DVIE_CHECK_ARG(x && out && n > 0, "sum_f32: args");
-  hipLaunchKernelGGL(sum_f32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, x, n, out);
+  DVIE_LAUNCH(sum_f32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, x, n, out);
   DVIE_RETURN_LAUNCH();
 }
 

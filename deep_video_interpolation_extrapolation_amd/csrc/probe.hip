@@ -66,6 +66,6 @@ using namespace dvie;
 
 extern "C" int dvie_mfma_probe(float* out, int blocks, int iters, void* stream) {
   DVIE_CHECK_ARG(out && blocks > 0 && iters > 0, "mfma_probe: args");
-  hipLaunchKernelGGL(mfma_probe_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, iters);
+  DVIE_LAUNCH(mfma_probe_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, iters);
   DVIE_RETURN_LAUNCH();
 }

@@ -225,7 +225,7 @@ extern "C" int dvie_segenc_fwd(const dvie_segenc_desc* d, void* stream) {
   const long long nt = (long long)tiles_x * tiles_y * d->n;
   DVIE_CHECK_ARG(nt < (1LL << 30), "segenc: too many tiles");
   const int grid = (int)(nt < 256 ? nt : 256);  // one 147-KB workgroup per CU, tiles round-robin
-  hipLaunchKernelGGL(segenc_fwd_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y, (int)nt);
+  DVIE_LAUNCH(segenc_fwd_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y, (int)nt);
   DVIE_RETURN_LAUNCH();
 }
 
@@ -575,7 +575,7 @@ extern "C" int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream) {
   const int tiles_x = (d->w + 63) / 64, tiles_y = (d->h + 3) / 4;
   const long long nt = (long long)tiles_x * tiles_y * d->n;
   DVIE_CHECK_ARG(nt < (1LL << 30), "segenc_bwd: too many tiles");
-  hipLaunchKernelGGL(segenc_bwd_kernel, dim3(d->slabs), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y,
+  DVIE_LAUNCH(segenc_bwd_kernel, dim3(d->slabs), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y,
                      (int)nt);
   DVIE_RETURN_LAUNCH();
 }

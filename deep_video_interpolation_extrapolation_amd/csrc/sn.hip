@@ -151,9 +151,9 @@ static int sn_launch(const dvie_sn_layer* layers, int n, const float* state, hip
       if (need > lds) lds = need;
     }
     if (bwd)
-      hipLaunchKernelGGL(sn_bwd_kernel, dim3(cnt), dim3(SN_THREADS), lds, st, b, state);
+      DVIE_LAUNCH(sn_bwd_kernel, dim3(cnt), dim3(SN_THREADS), lds, st, b, state);
     else
-      hipLaunchKernelGGL(sn_fwd_kernel, dim3(cnt), dim3(SN_THREADS), lds, st, b, (float*)state);
+      DVIE_LAUNCH(sn_fwd_kernel, dim3(cnt), dim3(SN_THREADS), lds, st, b, (float*)state);
   }
   return DVIE_OK;
 }

@@ -37,7 +37,7 @@ extern "C" {
 int dvie_reparam_fwd(const float* mu, const float* logvar, const float* eps, float* z, long long n, void* stream) {
   DVIE_CHECK_ARG(mu && logvar && eps && z && n >= 0, "reparam fwd: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(reparam_fwd_kernel, dim3(vae_grid(n)), dim3(256), 0, (hipStream_t)stream, mu, logvar, eps, z, n);
+  DVIE_LAUNCH(reparam_fwd_kernel, dim3(vae_grid(n)), dim3(256), 0, (hipStream_t)stream, mu, logvar, eps, z, n);
   DVIE_RETURN_LAUNCH();
 }
 
@@ -45,7 +45,7 @@ int dvie_reparam_bwd(const float* logvar, const float* eps, const float* gz, flo
                      int beta, void* stream) {
   DVIE_CHECK_ARG(logvar && eps && gz && gmu && glogvar && n >= 0, "reparam bwd: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(reparam_bwd_kernel, dim3(vae_grid(n)), dim3(256), 0, (hipStream_t)stream, logvar, eps, gz, gmu,
+  DVIE_LAUNCH(reparam_bwd_kernel, dim3(vae_grid(n)), dim3(256), 0, (hipStream_t)stream, logvar, eps, gz, gmu,
                      glogvar, n, beta);
   DVIE_RETURN_LAUNCH();
 }

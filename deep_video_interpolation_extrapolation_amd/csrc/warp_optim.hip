@@ -556,13 +556,13 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   const char* xe = getenv("DVIE_WARP_XCD");
   const int xcd = xe && *xe ? atoi(xe) : ((long long)d->n * d->c * d->h * d->w * 4 > (64ll << 20));
   if (d->c == 3 && ntm == 1)
-    hipLaunchKernelGGL((warp_fwd_kernel<3, 0, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
+    DVIE_LAUNCH((warp_fwd_kernel<3, 0, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else if (d->c == 3 && ntm == 2)
-    hipLaunchKernelGGL((warp_fwd_kernel<3, 2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
+    DVIE_LAUNCH((warp_fwd_kernel<3, 2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else if (d->c == 3)
-    hipLaunchKernelGGL(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
+    DVIE_LAUNCH(warp_fwd_kernel<3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else
-    hipLaunchKernelGGL(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
+    DVIE_LAUNCH(warp_fwd_kernel<0>, dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   DVIE_RETURN_LAUNCH();
 }
 
@@ -589,23 +589,23 @@ int dvie_warp_bwd(const dvie_warp_desc* d, void* stream) {
   const int grid = (int)std::min<long long>((waves + 3) / 4, 16384);
   const bool c3 = d->c == 3;
   if (c3)
-    hipLaunchKernelGGL(warp_bwd_tap_kernel<3>, dim3(grid), dim3(256), 0, s, *d);
+    DVIE_LAUNCH(warp_bwd_tap_kernel<3>, dim3(grid), dim3(256), 0, s, *d);
   else
-    hipLaunchKernelGGL(warp_bwd_tap_kernel<0>, dim3(grid), dim3(256), 0, s, *d);
+    DVIE_LAUNCH(warp_bwd_tap_kernel<0>, dim3(grid), dim3(256), 0, s, *d);
   if (d->dimg) {
     if (warp_win_env == 3) {
       if (c3)
-        hipLaunchKernelGGL((warp_bwd_pull_kernel<3, 3>), dim3(grid), dim3(256), 0, s, *d);
+        DVIE_LAUNCH((warp_bwd_pull_kernel<3, 3>), dim3(grid), dim3(256), 0, s, *d);
       else
-        hipLaunchKernelGGL((warp_bwd_pull_kernel<3, 0>), dim3(grid), dim3(256), 0, s, *d);
+        DVIE_LAUNCH((warp_bwd_pull_kernel<3, 0>), dim3(grid), dim3(256), 0, s, *d);
     } else {
       if (c3)
-        hipLaunchKernelGGL((warp_bwd_pull_kernel<4, 3>), dim3(grid), dim3(256), 0, s, *d);
+        DVIE_LAUNCH((warp_bwd_pull_kernel<4, 3>), dim3(grid), dim3(256), 0, s, *d);
       else
-        hipLaunchKernelGGL((warp_bwd_pull_kernel<4, 0>), dim3(grid), dim3(256), 0, s, *d);
+        DVIE_LAUNCH((warp_bwd_pull_kernel<4, 0>), dim3(grid), dim3(256), 0, s, *d);
     }
     const long long quads = ((long long)d->n * d->h * d->w + 3) / 4;
-    hipLaunchKernelGGL(warp_bwd_far_kernel, dim3((unsigned)std::min<long long>((quads + 255) / 256, 4096)), dim3(256), 0, s, *d);
+    DVIE_LAUNCH(warp_bwd_far_kernel, dim3((unsigned)std::min<long long>((quads + 255) / 256, 4096)), dim3(256), 0, s, *d);
   }
   DVIE_RETURN_LAUNCH();
 }
@@ -614,7 +614,7 @@ int dvie_adamax(float* p, const float* g, float* m, float* u, long long n, float
                 float wd, void* stream) {
   DVIE_CHECK_ARG(p && g && m && u && n >= 0, "adamax: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(adamax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, u, n, clr, b1, b2,
+  DVIE_LAUNCH(adamax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, u, n, clr, b1, b2,
                      eps, wd, (const float*)nullptr, 0.0, 0.0);
   DVIE_RETURN_LAUNCH();
 }
@@ -623,21 +623,21 @@ int dvie_adamax_dev(float* p, const float* g, float* m, float* u, long long n, d
                     double eps, double wd, const float* step, void* stream) {
   DVIE_CHECK_ARG(p && g && m && u && step && n >= 0, "adamax_dev: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(adamax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, u, n, 0.f,
+  DVIE_LAUNCH(adamax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, g, m, u, n, 0.f,
                      (float)b1, (float)b2, (float)eps, (float)wd, step, lr, b1);
   DVIE_RETURN_LAUNCH();
 }
 
 int dvie_step_inc(float* step, void* stream) {
   DVIE_CHECK_ARG(step, "step_inc: null");
-  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step);
+  DVIE_LAUNCH(step_inc_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step);
   DVIE_RETURN_LAUNCH();
 }
 
 int dvie_scale(float* p, long long n, float s, void* stream) {
   DVIE_CHECK_ARG(p && n >= 0, "scale: args");
   if (n == 0) return DVIE_OK;
-  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, n, s);
+  DVIE_LAUNCH(scale_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, n, s);
   DVIE_RETURN_LAUNCH();
 }
 

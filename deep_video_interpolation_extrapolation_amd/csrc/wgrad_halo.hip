@@ -640,17 +640,17 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   const int grid = n_co * n_ci * p.splits;
   const bool wg_pipe = wg_pipe_on();
   if (w.wide) {
-    hipLaunchKernelGGL(wgrad_wide_kernel, dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, n_tiles);
+    DVIE_LAUNCH(wgrad_wide_kernel, dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, n_tiles);
     return true;
   }
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
-  hipLaunchKernelGGL((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
+  DVIE_LAUNCH((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
                      tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio | wg_dbg())
   if (p.th == 3 && p.cout > 32 && wg_pipe)
-    hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
+    DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio | wg_dbg());
   else if (p.th == 3 && p.cout <= 32 && !wg_narrow_env_off)
-    hipLaunchKernelGGL((wgrad_halo_kernel<3, 3, 4, 1, 1, 4>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
+    DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 4>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   else if (p.th == 3)
     DVIE_WG(3, 4, 1, 1);

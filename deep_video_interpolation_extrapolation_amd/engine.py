@@ -35,15 +35,17 @@ def _wgrad_lane():
     return os.environ.get("DVIE_WGRAD_LANE", "1") != "0"
 
 
+# test support: hook(plan, arr, i, meta, run) is handed every executed op and calls run() to
+# launch it (layer-local parity checks, tests/test_gpu_layers.py); None in the product
+OP_HOOK = None
+
+
 def pack_blocks(d):
-    """workgroups dvie_pack_weights gives descriptor d: the kinds of csrc/conv.hip pack_kind
-    (ROW: one per packed row, TILE: 8 rows x 64 columns, ELEM: 1024 elements)"""
-    if d.kpad >= 64 and d.kpad % 4 == 0:
-        if d.mode == 0 and d.cin_s * d.kh_s * d.kw_s <= 8192:
-            return d.rows
-        if d.mode == 1 and d.kh_s * d.kw_s <= 16 and d.c % 4 == 0:
-            return -(-d.rows // 8) * -(-d.c // 64)
-    return -(-d.rows * d.kpad // 1024)
+    """workgroups dvie_pack_weights gives descriptor d (the library's own count: its block
+    kinds are a function of the descriptor, csrc/conv.hip pack_kind)"""
+    n = L.load().dvie_pack_blocks(ctypes.byref(d))
+    assert n > 0, "dvie_pack_blocks: empty pack descriptor"
+    return n
 
 
 def _reduce_meta(name, r):
@@ -613,8 +615,12 @@ class Plan:
                 else:
                     need = any(r.buf.needs_grad for r in op.inputs())
                 op.out.buf.needs_grad = op.out.buf.needs_grad or need
+            # the hidden maps of a segmentation encoder whose backward is one dvie_segenc_bwd
+            # launch get no gradient storage: d_e1 / d_e2 stay on chip in that kernel
+            self._seg_bwd = self._segenc_bwd_chains()
+            self._seg_inner = {id(op.out.buf) for ch in self._seg_bwd.values() for op in ch[:2]}
             for b in g.buffers:
-                if b.needs_grad:
+                if b.needs_grad and id(b) not in self._seg_inner:
                     b.g = torch.zeros((self.nb, b.H, b.W, b.C), dtype=self.dtype, device=self.device)
             for b in g.buffers:
                 b.expected = {}
@@ -1188,12 +1194,13 @@ class Plan:
                 self.completions.append((len(self.bwd), lay))
         for op in (o0, o1):  # their output gradients are never formed (d_e1 / d_e2 stay on chip)
             op.out.buf.done = True
+            op.out.buf.dact_done = True
             op.out.buf.pending = {}
 
     def _build_backward(self):
         g = self.g
         nb = self.nb
-        seg_bwd = self._segenc_bwd_chains()
+        seg_bwd = self._seg_bwd
         seg_skip = {id(op) for ch in seg_bwd.values() for op in ch[:2]}
         self.wg_first = {}
         self.completions = []  # (bwd index, layer): the layer's parameter gradients are final
@@ -1253,6 +1260,8 @@ class Plan:
             b = out.buf
             if not b.needs_grad or not getattr(b, "done", False):
                 continue  # no gradient reaches this op
+            if id(op) in seg_skip:
+                continue  # inside a fused encoder backward: its gradient is never formed
             self._ensure_dact(op)
             gout, gld = self.ptr(out, grad=True), b.C
             if isinstance(op, InputOp):
@@ -1266,8 +1275,6 @@ class Plan:
                 continue
             if id(op) in seg_bwd:
                 self._segenc_backward(seg_bwd[id(op)], gout, gld)
-                continue
-            if id(op) in seg_skip:
                 continue
             if isinstance(op, ConvOp):
                 self._conv_backward(op, gout, gld)
@@ -1869,6 +1876,11 @@ class Plan:
                           f"{sorted(now - seen)}", flush=True)
                     seen = now
             return
+        if OP_HOOK is not None:  # op by op, each handed to the hook (which runs it)
+            for i in range(start, end):
+                OP_HOOK(self, arr, i, metas[i] if metas else None,
+                        lambda i=i: L.check(lib.dvie_run_ops(base + i * sz, 1, s), what))
+            return
         if PROFILE is None:
             L.check(lib.dvie_run_ops(base + start * sz, end - start, s), what)
             return
@@ -1880,6 +1892,11 @@ class Plan:
             e1.record()
             arr[i].lane = lane
             PROFILE.append((metas[i] if metas is not None else None, arr[i].kind, e0, e1))
+
+    def invalidate_pack(self):
+        """static_weights plans: repack at the next forward whatever the parameters' version
+        counters say (a write through p.data bumps none)."""
+        self._pack_sig = None
 
     def run_forward(self, stream=None):
         s = L.stream_ptr() if stream is None else stream

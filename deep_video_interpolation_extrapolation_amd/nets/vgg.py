@@ -124,6 +124,25 @@ class my_vgg(nn.Module):
         plan.feats = feats
         return plan
 
+    def invalidate_packs(self):
+        """Repack every plan's weights at its next forward.  The packed-weight cache keys on
+        (storage, version counter) of the parameters; a write through `p.data` (p.data.copy_,
+        a common way to load weights) bumps no version counter, so call this after one."""
+        pool = self.__dict__.get("_pool")
+        for plans in (pool.plans.values() if pool is not None else ()):
+            for p in plans:
+                p.invalidate_pack()
+
+    def load_state_dict(self, *args, **kwargs):
+        out = super().load_state_dict(*args, **kwargs)
+        self.invalidate_packs()
+        return out
+
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        self.invalidate_packs()
+        return out
+
     # -- loss execution (VGGLoss) --
     def run_forward(self, inputs, train):
         pred, gt, normalize = inputs[0], inputs[1], self._normalize

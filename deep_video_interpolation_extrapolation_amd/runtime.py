@@ -180,8 +180,13 @@ class PlanFunction(torch.autograd.Function):
         inputs = ctx.saved_tensors
         # parameters get a gradient only if they required one at the forward (autograd's rule:
         # a later requires_grad_(True) does not reach back into this graph)
+        # (read by runners during this call only: cleared afterwards, so a later run_backward
+        # outside PlanFunction never sees this graph's flags)
         ctx.runner._param_needs = tuple(ctx.needs_input_grad[2 + ctx.n_in:])
-        in_grads = ctx.runner.run_backward(plan, inputs, grads, ctx.needs_input_grad[2:2 + ctx.n_in])
+        try:
+            in_grads = ctx.runner.run_backward(plan, inputs, grads, ctx.needs_input_grad[2:2 + ctx.n_in])
+        finally:
+            ctx.runner._param_needs = None
         plan.busy = False
         ctx.token = None
         return (None, None) + tuple(in_grads) + (None,) * ctx.n_params

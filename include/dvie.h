@@ -180,6 +180,10 @@ typedef struct dvie_pack_desc {
 
 int dvie_pack_weights(const dvie_pack_desc* descs_dev, int n, int blocks, void* stream);
 
+/* Number of flat-grid blocks dvie_pack_weights gives descriptor d (host memory): the blk0 of
+ * the next descriptor is d->blk0 plus this, and `blocks` is the sum over all descriptors. */
+int dvie_pack_blocks(const dvie_pack_desc* d);
+
 /*
  * Pointwise NHWC family (4 channels per thread).  op selects:
  *  DVIE_EW_FUSE   y = act( sum_i up_i(src_i) ) — HighResolutionModule fuse sum
@@ -727,6 +731,14 @@ size_t dvie_abi_sizeof(int which);
 const char* dvie_version(void);
 /* last error text of the calling thread (argument validation) */
 const char* dvie_last_error(void);
+
+/* Diagnostics (tests, profiling): launch trace of the calling thread.  dvie_trace_kernels(1)
+ * starts recording the kernels every entry point of this thread launches (0 stops; both clear
+ * the record; returns the previous state).  dvie_traced_kernels() returns the demangled names
+ * of the kernels launched since the last call, ';'-separated in launch order, and clears the
+ * record (the text stays valid until the thread's next call). */
+int dvie_trace_kernels(int on);
+const char* dvie_traced_kernels(void);
 
 #ifdef __cplusplus
 }

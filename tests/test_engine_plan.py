@@ -172,3 +172,34 @@ def test_weight_lane_tags(dtype, monkeypatch):
                 assert o.lane == 0, o.kind
         assert n_w > 50
         assert all(plan.fwd_arr[i].lane == 0 for i in range(len(plan.fwd_arr)))
+
+
+def test_fused_segenc_backward_leaves_no_dead_work():
+    """bf16 HRNet plan with the fused segmentation-encoder backward (dvie_segenc_bwd): the
+    encoder's hidden maps e1 / e2 get no gradient storage (d_e1 / d_e2 stay on chip in that
+    kernel), and no backward op applies an ELU derivative to a gradient nobody reads (the
+    r04 plan emitted one such EW_COPY per map and frame)."""
+    hr = make().coarse_model
+    g = hr._lower(E.Graph(torch.bfloat16), 32, 64)
+    plan = g.compile(2, torch.device("cpu"), backward=True)
+    assert plan.describe()["kinds"].get(L.OP_SEGENC_BWD, 0) == 2
+    inner = [b for b in g.buffers if b.name.startswith("seg") and b.name.endswith(("_e1", "_e2"))]
+    assert len(inner) == 4 and all(b.g is None for b in inner)
+    for i in range(plan.n_bwd):
+        o = plan.bwd_arr[i]
+        if o.kind == L.OP_EW:
+            assert o.u.ew.dact != L.ACT_ELU, "an ELU derivative pass is left in the backward"
+
+
+def test_pack_blocks_from_the_library():
+    """The flat pack grid's per-descriptor block counts come from the library
+    (dvie_pack_blocks), and the descriptors' blk0 tile the grid."""
+    hr = make().coarse_model
+    g = hr._lower(E.Graph(torch.bfloat16), 32, 64)
+    plan = g.compile(2, torch.device("cpu"), backward=True)
+    descs = plan._pack_descs
+    blk = 0
+    for d in descs:
+        assert d.blk0 == blk
+        blk += L.load().dvie_pack_blocks(__import__("ctypes").byref(d))
+    assert plan.fwd_arr[0].u.pack.blocks == blk
