@@ -32,16 +32,19 @@ def synthetic_vgg19_state(seed=19):
     return state
 
 
-def gaussian_window(window_size=11, sigma=1.5):
+def gaussian_window(window_size=11, sigma=1.5, dtype=torch.float32):
+    """losses.py:18-26: the 1-D gaussian and its outer product are formed in the default dtype
+    (torch.Tensor(list)) -- `dtype` here: that of the images, so a float64 run builds it in float64
+    as the reference does under a float64 default -- then rounded to fp32 (`.float()`)"""
     g = torch.tensor([exp(-(x - window_size // 2) ** 2 / float(2 * sigma ** 2)) for x in range(window_size)],
-                     dtype=torch.float32)
+                     dtype=dtype)
     g = g / g.sum()
     return (g[:, None] @ g[None, :]).float()
 
 
 def ssim_value(img1, img2, window_size=11):
     c = img1.shape[1]
-    w = gaussian_window(window_size).to(img1.dtype).expand(c, 1, window_size, window_size).contiguous()
+    w = gaussian_window(window_size, dtype=img1.dtype).to(img1.dtype).expand(c, 1, window_size, window_size).contiguous()
     p = window_size // 2
     mu1 = F.conv2d(img1, w, padding=p, groups=c)
     mu2 = F.conv2d(img2, w, padding=p, groups=c)

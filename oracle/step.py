@@ -110,7 +110,7 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
              w_rgb=(80.0, 80.0, 20.0, 20.0), w_ce=30.0, w_d=1.0, w_g=1.0, state=None, masks=None, vmasks=None,
              gf_masks=None, gv_masks=None, dtype=torch.float32, frame_spec="FrameDiscriminator",
              video_spec="VideoDiscriminator", vae=None, kld_w=20.0, uv_grad=False, df_masks=(None, None),
-             dv_masks=(None, None), adam="1.0.1"):
+             dv_masks=(None, None), adam="1.0.1", grad_override=None):
     """One InterGANTrainer step (reference runners/InterGANTrainer.py:359-456 with
     nets/InterGANNet.py:28-117): frame and video discriminators with seg_disc; D(fake.detach())
     and D(real) train the discriminators, D(fake) with them frozen trains the generator; RGBLoss
@@ -133,7 +133,11 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
     (fake, real) discriminator passes, gf_masks / gv_masks: the frozen G passes).
     Returns (loss dict, new generator params, new frame disc params, new video disc params,
     state, grads); state["stats"] = (frame, video[, vae]) running statistics after the step and
-    the new u / v (post power iteration, post Adam) are in the new disc params."""
+    the new u / v (post power iteration, post Adam) are in the new disc params.
+    grad_override: {"g" / "f" / "v": {name: (flat indices, values)}} written into those gradients
+    before the optimizers (test support: a check against a fixture starts its next step from the
+    fixture's own signs of near-zero gradient elements, which a first Adamax / Adam step turns into
+    +-lr moves whatever their size)."""
     from . import disc as D
     from . import vaehrnet as V
     P = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in params.items()}
@@ -176,6 +180,9 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
         loss = loss + torch.mean(v)
     ld["loss_all"] = loss
     loss.backward()
+    for tag, Pd in (("g", P), ("f", Pf), ("v", Pv)):
+        for name, (idx, vals) in (grad_override or {}).get(tag, {}).items():
+            Pd[name].grad.view(-1)[idx] = vals.to(Pd[name].grad.dtype)
     st = state or {}
 
     def cur(src, Pd):  # u / v as the power iterations left them

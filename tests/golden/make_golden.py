@@ -35,7 +35,11 @@ data only (inputs are regenerated from seeds by tests/golden/inputs.py; outputs 
                      VAEHRNet coarse model (KLD term) and FrameSN / VideoSN discriminators
                      (seg_disc), 128x128, batch 2; step 2 with SpectralNorm u / v trainable
                      (set_net_grad(True)): loss dicts, gradient stats, post-step checksums, u / v,
-                     BatchNorm running statistics
+                     BatchNorm running statistics, 64 seeded elements of every gradient and every
+                     post-step tensor, the post-step values of the BatchNorm-preceding biases
+  gan_vae64.npz  G14d: the same two steps with the reference modules widened to float64 after
+                     their seeded fp32 initialisation (float64 draws after that), the same
+                     records plus step 1's near-zero gradient elements (index, value)
 """
 import os
 import sys
@@ -352,6 +356,32 @@ def _gstats(module):
                                       for n in names])
 
 
+def _samples(module_or_sd, names, grad):
+    """64 seeded elements of each named gradient (grad=True) or state tensor, in names order
+    (inputs.sample_idx(numel, 64): fixed positions per tensor size)"""
+    src = dict(module_or_sd.named_parameters()) if grad else module_or_sd
+    rows = []
+    for n in names:
+        t = src[str(n)].grad if grad else src[str(n)]
+        v = t.detach().double().reshape(-1)
+        rows.append(v[inputs.sample_idx(v.numel(), 64)].numpy())
+    return np.array(rows)
+
+
+def _small_grads(module, names, rel=1e-5):
+    """(tensor index, flat index, value) of every gradient element with 0 < |g| <= rel * max|g| of
+    its tensor: the elements whose sign rounding can decide (Adamax / Adam take a first step of
+    +-lr whatever |g| is), so a check can start its next step from the reference's own signs"""
+    named = dict(module.named_parameters())
+    rows = []
+    for i, n in enumerate(names):
+        g = named[str(n)].grad.detach().double().reshape(-1)
+        m = (g != 0) & (g.abs() <= rel * float(g.abs().max()))
+        idx = torch.nonzero(m).reshape(-1)
+        rows += [[i, int(j), float(g[j])] for j in idx]
+    return np.array(rows, dtype=np.float64).reshape(-1, 3)
+
+
 def _flat_sample(t):
     v = t.detach().double().reshape(-1)
     return np.concatenate([[float(v.sum()), float(v.abs().sum()), float(v.norm())],
@@ -407,7 +437,7 @@ def g12():
     np.savez_compressed(os.path.join(HERE, "clip_crops.npz"), crops=np.array(crops), flips=np.array(flips))
 
 
-def g14():
+def g14(dtype=torch.float32, fname="gan_vae.npz"):
     """The reference's InterGAN step body composed from its own modules (InterGANNet forward,
     RGBLoss on (x + 1) / 2, 30 * CrossEntropy, KLDLoss, GANScalarLoss, Adamax / Adam), W = 1.
     The reparameterisation noise of step k is the CPU draw right after torch.manual_seed(78 + k)
@@ -418,9 +448,13 @@ def g14():
                    video_disc_model="VideoSNDiscriminator", seg_disc=True, rank=0, kld_weight=20.0, vae=True)
     cuda0 = torch.Tensor.cuda
     torch.Tensor.cuda = lambda self, *a, **k: self
+    dt0 = torch.get_default_dtype()
     try:
         torch.manual_seed(1024)
         model = ref_nets.InterGANNet(args)
+        if dtype != torch.float32:  # float64 run (G14d): the same seeded fp32 init, then widened
+            torch.set_default_dtype(dtype)
+            model = model.to(dtype)
         model.train()
         rgb_loss = ref_losses.RGBLoss(args)
         kld = ref_losses.KLDLoss(args)
@@ -433,6 +467,7 @@ def g14():
         for mod, tag in ((model.coarse_model, "g"), (model.frame_disc_model, "f"), (model.video_disc_model, "v")):
             out[tag + "_init_names"], out[tag + "_init"] = checksums(dict(mod.state_dict()))
         data = inputs.step_batch(2, 128, 128)
+        data = {k: (v.to(dtype) if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in data.items()}
         for k in range(2):
             gt_x, gt_seg = data["frame2"], data["seg2"]
             x = torch.cat([data["frame1"], data["frame3"]], dim=1)
@@ -463,18 +498,40 @@ def g14():
             out[t + "loss_values"] = np.array([float(v) for v in ld.values()])
             for mod, tag in ((model.coarse_model, "g"), (model.frame_disc_model, "f"), (model.video_disc_model, "v")):
                 out[t + tag + "_grad_names"], out[t + tag + "_grad_stats"] = _gstats(mod)
+                out[t + tag + "_grad_samples"] = _samples(mod, out[t + tag + "_grad_names"], True)
+                if dtype != torch.float32 and k == 0:
+                    out[t + tag + "_grad_small"] = _small_grads(mod, out[t + tag + "_grad_names"])
             for o in (coarse_opt, frame_opt, video_opt):
                 o.step()
             for mod, tag in ((model.coarse_model, "g"), (model.frame_disc_model, "f"), (model.video_disc_model, "v")):
                 out[t + tag + "_post_names"], out[t + tag + "_post"] = checksums(dict(mod.state_dict()))
-        np.savez_compressed(os.path.join(HERE, "gan_vae.npz"), **out)
+                sd = dict(mod.state_dict())
+                out[t + tag + "_post_samples"] = _samples(sd, out[t + tag + "_post_names"], False)
+            # the conv biases right before a train-mode BatchNorm get a rounding-noise gradient (true
+            # value 0) that Adamax turns into +-lr steps: their whole post-step values, so a check of
+            # the next step can start from the reference's own
+            sd = dict(model.coarse_model.state_dict())
+            bn_b = sorted(n for n in sd if n.endswith(".bias") and "." in n[:-5] and n[:-5].rsplit(".", 1)[1].isdigit()
+                          and f"{n[:-5].rsplit('.', 1)[0]}.{int(n[:-5].rsplit('.', 1)[1]) + 1}.running_mean" in sd)
+            out[t + "g_bnbias_names"] = np.array(bn_b)
+            out[t + "g_bnbias_post"] = np.concatenate([sd[n].detach().double().reshape(-1).numpy() for n in bn_b])
+        np.savez_compressed(os.path.join(HERE, fname), **out)
     finally:
         torch.Tensor.cuda = cuda0
+        torch.set_default_dtype(dt0)
+
+
+def g14d():
+    """G14 in float64 (gan_vae64.npz): the same two steps with the reference modules widened to
+    float64 after their seeded fp32 initialisation, so a per-tensor comparison with the float64
+    oracle sees the algorithm, not fp32 rounding (which the VAE decoder's gradients amplify about
+    100x by the second step: the oracle's own fp32 and fp64 runs differ by 2.4e-4 there)."""
+    g14(torch.float64, "gan_vae64.npz")
 
 
 if __name__ == "__main__":
     import sys as _sys
-    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11, g12, g14)}
+    todo = {f.__name__: f for f in (g1, g2, g3, g5, g4, g6, g7, g8, g9, g10, g11, g12, g14, g14d)}
     for name in (_sys.argv[1:] or list(todo)):
         f = todo[name]
         f()

@@ -111,3 +111,83 @@ def test_gan_vae_sn_two_steps_match_reference(monkeypatch):
             # elements (one BatchNorm beta, 32 elements, measured 2.5e-3); the median stays ~1e-8
             _check_sumsq(post[tag], np.array(names), f[t + tag + "_post"][idx], (1e-5, 1e-4 if k == 0 else 5e-3),
                          t + tag + " post")
+
+
+# ---- G14d: the same two steps in float64, compared per tensor ----
+# Per-tensor bar: relative L2 over 64 seeded elements (inputs.sample_idx) of every gradient and
+# every post-step tensor <= 1e-6 (measured worst 9.7e-8 gradients, 2.8e-7 post-step; loss values
+# 1.8e-8), loss values 1e-7.  In fp32 the same comparison is bounded by rounding that the VAE
+# decoder amplifies ~100x by step 2 (the fp32 fixture's checks above); in float64 only the
+# algorithm is left.  Exclusions, each listed (tests/golden/make_golden.py g14d):
+# * the 17 conv biases right before a train-mode BatchNorm (_bn_biases): true gradient exactly 0,
+#   so both sides hold rounding noise, which Adamax's sign-like first step turns into +-lr moves
+#   of their post-step values;
+# * from step 2 on, the running means of those BatchNorms (they average the biases' +-lr moves);
+# * and no tensor, but step 1's near-zero gradient elements are set to the reference's values
+#   before the optimizers (below): without that the same check gives 2.1e-6 / 6.4e-6 at step 2.
+G14D_BAR = 1e-6
+
+
+def _rel_samples(t, ref):
+    v = t.detach().double().reshape(-1)
+    got = v[inputs.sample_idx(v.numel(), 64)].numpy()
+    return float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-300))
+
+
+def test_gan_vae_sn_two_steps_match_reference_float64_per_tensor(monkeypatch):
+    monkeypatch.setattr(OD, "SN_PER_CALL", False)  # (as above: this container's torch semantics)
+    f = np.load(os.path.join(G, "gan_vae64.npz"))
+    sg, sf, sv = (({k: v.double() for k, v in sd.items()}) for sd in reference_init())
+    dt0 = torch.get_default_dtype()
+    # the draws the float64 generator made after widening the model (the VGG stand-in, the batch,
+    # the reparameterisation noise) were float64 draws
+    torch.set_default_dtype(torch.float64)
+    try:
+        vs = OL.synthetic_vgg19_state()
+        data = inputs.step_batch(2, 128, 128)
+        eps = [inputs.vae_eps(2, 78 + k) for k in range(2)]
+    finally:
+        torch.set_default_dtype(dt0)
+    Pg, Pf, Pv = _params(sg), _params(sf), _params(sv)
+    vae_stats = V.bn_stats(sg)
+    bn = _bn_biases(sg)
+    # step 1's near-zero gradient elements (0 < |g| <= 1e-5 max|g| of their tensor) take the
+    # reference's own values before the optimizers: both first steps move every element by +-lr
+    # whatever |g| is, and at fp64 rounding 10 of the generator's 12.7 M elements (|g| ~ 1e-10 of
+    # a 5e-4 maximum) come out with the other sign -- each then 2e-3 apart, which moved step 2's
+    # losses by up to 5e-6
+    override = {}
+    for tag in ("g", "f", "v"):
+        names = [str(n) for n in f[f"step1_{tag}_grad_names"]]
+        rows = f[f"step1_{tag}_grad_small"]
+        ov = {}
+        for i in sorted({int(r) for r in rows[:, 0]}):
+            sel = rows[rows[:, 0] == i]
+            ov[names[i]] = (torch.from_numpy(sel[:, 1].astype(np.int64)), torch.from_numpy(sel[:, 2]))
+        override[tag] = ov
+    state, worst = None, {}
+    for k in range(2):
+        t = f"step{k + 1}_"
+        ld, Pg, Pf, Pv, state, grads = OS.gan_step(Pg, Pf, Pv, vs, data, {}, {}, frame_spec=FRAME, video_spec=VIDEO,
+                                                   vae={"eps": eps[k], "stats": vae_stats}, uv_grad=k > 0,
+                                                   state=state, adam="torch2", dtype=torch.float64,
+                                                   grad_override=override if k == 0 else None)
+        vae_stats = state["stats"][2]
+        loss_err = np.abs(np.array(list(ld.values())) - f[t + "loss_values"]) / np.abs(f[t + "loss_values"])
+        worst[t + "loss"] = (float(loss_err.max()), str(f[t + "loss_names"][int(loss_err.argmax())]), float(np.median(loss_err)))
+        skip = set(bn) | ({f"{b.rsplit('.', 2)[0]}.{int(b.rsplit('.', 2)[1]) + 1}.running_mean" for b in bn}
+                          if k > 0 else set())
+        post = {"g": dict(Pg, **{n + ".running_mean": m for n, (m, _) in vae_stats.items()},
+                          **{n + ".running_var": v for n, (_, v) in vae_stats.items()}), "f": Pf, "v": Pv}
+        for tag in ("g", "f", "v"):
+            for kind, src in (("grad", grads[tag]), ("post", post[tag])):
+                names = [str(n) for n in f[t + tag + f"_{kind}_names"]]
+                S = f[t + tag + f"_{kind}_samples"]
+                errs = {n: _rel_samples(src[n], S[i]) for i, n in enumerate(names)
+                        if n not in skip and "num_batches" not in n}
+                w = max(errs, key=errs.get)
+                worst[t + tag + "_" + kind] = (errs[w], w, float(np.median(list(errs.values()))))
+    for key, (e, n, med) in worst.items():
+        print(f"G14d {key}: worst {e:.2e} ({n}), median {med:.2e}")
+    for key, (e, n, med) in worst.items():
+        assert e <= (1e-7 if key.endswith("loss") else G14D_BAR), (key, n, e)
