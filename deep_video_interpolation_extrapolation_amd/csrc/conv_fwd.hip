@@ -362,6 +362,7 @@ static void dispatch_conv(const dvie_conv_desc& p, hipStream_t s) {
 
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_halo.hip
 bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s);    // conv1x1.hip
+bool conv_s2_launch(const dvie_conv_desc& p, hipStream_t s);    // conv_s2.hip
 
 }  // namespace dvie
 
@@ -405,6 +406,7 @@ extern "C" int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
     if (d->z) c.z = (const char*)d->z + n0 * img_y * d->z_ld * es;
     if (conv1x1_launch(c, s)) continue;
     if (conv_halo_launch(c, s)) continue;
+    if (conv_s2_launch(c, s)) continue;
     if (c.dtype == DVIE_BF16)
       dispatch_conv<bf16_t>(c, s);
     else

@@ -1,0 +1,352 @@
+// Stride-2 3x3 forward convolution (zero padding 1) for gfx950, bf16: HRNet's downsampling
+// convs -- transition1.1 / transition2.2 and the strided fuse-layer chains (reference
+// nets/HRNet.py:166-194 fuse_layers, l.444-477 transition layers).
+//
+// Phase-split halo.  A workgroup owns PR = 4 output rows x 64 output pixels x BC output
+// channels.  Its input region, (2 PR + 1) rows x 129 columns, is staged once per 16-channel
+// chunk by LDS-DMA, each input row split into its even and its odd columns (two "phase rows"
+// of 65 pixels): output pixel j's tap (ti, tj) reads input column 2j + tj - 1, i.e. pixel
+// j + (tj >> 1) of phase row tj & 1, so the B fragment of a tap for 32 consecutive output
+// pixels is 32 consecutive pixels of one phase row -- a stride-1 read, as in the stride-1
+// halo kernels, and the input is fetched once per chunk instead of once per tap (the per-tap
+// implicit GEMM of conv_fwd.hip gathered it nine times from L2).  Pixel pitch 48 B (16
+// channels + a 16-B pad slot, DMA'd as zeros): any 16 consecutive pixels' b128 reads hit 16
+// distinct bank quads.
+//   Weights stream one tap COLUMN (3 taps, BC rows x 32 B each, 16-B chunks XOR-swizzled by
+// (row >> 3) & 1) per step, double buffered; the next chunk's halo is issued in two shares
+// under the current chunk's first two columns.  One vmcnt wait + barrier per column.
+//   8 waves = 2 (output-channel halves of 32 TM) x 4 (output rows); a wave owns 32 TM
+// channels x 1 row x 64 pixels (2 TM accumulators of 32 x 32).  LDS: 2 x 56 KB halo +
+// 2 column buffers (8 / 16 / 24 KB for TM = 1 / 2 / 4): one workgroup per CU, persistent
+// over an XCD-contiguous tile range.  Epilogue from registers: bias, residual (EPI bit 1),
+// activation.
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+namespace dvie {
+
+typedef __attribute__((address_space(3))) void* lds_ptr_s2;
+
+// vmcnt(N) and lgkmcnt(0)
+#define DVIE_S2_VMCNT_LGKM0(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4))
+
+__device__ __forceinline__ uint32_t s2_pack(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
+}
+
+template <int TM>
+struct S2 {
+  static constexpr int NW = 8, NTH = 512;
+  static constexpr int BC = 64 * TM, PR = 4, KC = 16;
+  static constexpr int HR = 2 * PR + 1, HP = 65;  // halo rows; pixels per phase row
+  static constexpr int PITCH = 48;                 // 32 data bytes + a 16-B pad slot
+  static constexpr int RSLOTS = 2 * HP * 3;        // 16-B slots per input row (two phase rows)
+  static constexpr int HSLOTS = HR * RSLOTS;
+  static constexpr int NHI = ((HSLOTS + 63) / 64 + NW - 1) / NW * NW;
+  static constexpr int NHQ = NHI / NW;             // halo pieces per wave per chunk
+  static constexpr int HSZ = NHI * 1024;
+  static constexpr int TSZ = BC * 32;              // one tap of one chunk: BC rows x 32 B
+  static constexpr int WPC = (3 * TSZ / 1024 + NW - 1) / NW;  // weight pieces per wave per column
+  static constexpr int WSZ = WPC * NW * 1024;      // one column buffer
+  static constexpr int SMEM = 2 * HSZ + 2 * WSZ;
+  static constexpr int H0 = 4;                     // halo pieces per wave issued in column 0 (rest: column 1)
+};
+static_assert(S2<4>::SMEM <= 163840 && S2<2>::SMEM <= 163840 && S2<1>::SMEM <= 163840, "conv_s2 LDS budget");
+static_assert(S2<2>::NHQ == 7 && S2<2>::H0 < S2<2>::NHQ, "halo shares");
+
+struct S2Job {
+  int valid, t, k, c0, n, y0, x0;
+};
+
+// halo pieces [qa, qb) of job J (a job past the end issues its pieces with an empty range: they
+// land as zeros nobody reads, and the vmcnt bookkeeping stays compile-time)
+template <int NW>
+__device__ __forceinline__ void s2_halo(const dvie_conv_desc& p, const S2Job& J, char* dst, const int* hgeo, int qa,
+                                        int qb, unsigned long long xbytes, unsigned xrow) {
+  const unsigned OOB = 0xFFFFFFF0u;
+  const int nrec = J.valid ? (int)(xbytes - (unsigned long long)J.k * 32) : 0;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + (size_t)J.k * 32), 0, nrec, 0x00020000);
+  const int ybase = 2 * J.y0 - 1, xbase = 2 * J.x0 - 1;
+#pragma unroll
+  for (int q = qa; q < qb; ++q) {
+    const int gq = hgeo[q];
+    const int iy = ybase + (gq >> 16), ix = xbase + ((gq >> 4) & 0xFFF);
+    const bool ok = gq >= 0 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw;
+    const unsigned o0 = (unsigned)((J.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)(gq & 15) * 16u;
+    const unsigned o = ok ? o0 : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_s2)(dst + q * NW * 1024), 16, o, 0, 0, 0);
+  }
+}
+
+template <int TM, int EPI>
+__global__ __launch_bounds__(512) void conv_s2_kernel(const dvie_conv_desc p, int n_ct, int n_tiles, int tiles_x,
+                                                      int tiles_y) {
+  typedef S2<TM> C;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave >> 2, wr = wave & 3;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nchunks = p.c >> 4;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  // persistent: XCD g (= blockIdx % 8) takes a contiguous tile range, its blocks stride it
+  const int G = gridDim.x, g = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int nbg = G / 8 + (g < G % 8 ? 1 : 0);
+  const int q8 = n_tiles / 8, r8 = n_tiles % 8;
+  const int ts = g < r8 ? g * (q8 + 1) : r8 * (q8 + 1) + (g - r8) * q8;
+  const int tile0 = ts + jb, tile_end = ts + q8 + (g < r8 ? 1 : 0);
+  if (tile0 >= tile_end) return;
+
+  auto tile_job = [&](int t) {
+    S2Job J;
+    J.t = t;
+    J.k = 0;
+    J.valid = t < tile_end;
+    J.c0 = (t % n_ct) * C::BC;
+    int pt = t / n_ct;
+    J.x0 = (pt % tiles_x) * 64;
+    pt /= tiles_x;
+    J.y0 = (pt % tiles_y) * C::PR;
+    J.n = pt / tiles_y;
+    return J;
+  };
+  auto next_job = [&](const S2Job& J) {
+    if (J.k + 1 < nchunks) {
+      S2Job N = J;
+      N.k = J.k + 1;
+      return N;
+    }
+    return tile_job(J.t + nbg);
+  };
+
+  // halo DMA geometry: slot -> (input row hr, input column hc = 2 px + phase, 16-B group cs;
+  // group 2 = pad)
+  int hgeo[C::NHQ];
+#pragma unroll
+  for (int q = 0; q < C::NHQ; ++q) {
+    const int slot = (wave + C::NW * q) * 64 + lane;
+    const int hr = slot / C::RSLOTS, rem = slot - (slot / C::RSLOTS) * C::RSLOTS;
+    const int ph = rem / (3 * C::HP), rem2 = rem - ph * (3 * C::HP);
+    const int px = rem2 / 3, cs = rem2 - 3 * (rem2 / 3);
+    hgeo[q] = (cs < 2 && slot < C::HSLOTS) ? (hr << 16) | ((2 * px + ph) << 4) | cs : -1;
+  }
+  // weight DMA geometry: slot -> (tap row ti of the column, weight row, source chunk); the
+  // source offset without the per-issue terms (channel block, column, chunk), or OOB
+  unsigned woff[C::WPC];
+#pragma unroll
+  for (int q = 0; q < C::WPC; ++q) {
+    const int slot = (wave + C::NW * q) * 64 + lane;
+    const int ti = slot / (2 * C::BC), rem = slot - ti * (2 * C::BC);
+    const int row = rem >> 1, ch = (rem & 1) ^ ((row >> 3) & 1);
+    const unsigned wo = (unsigned)row * (unsigned)p.kpad * 2u + (unsigned)(ti * 3 * p.c + ch * 8) * 2u;
+    woff[q] = slot < 3 * 2 * C::BC ? wo : OOB;
+  }
+  const unsigned xrow = (unsigned)p.x_ld * 2u;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const unsigned wbytes = (unsigned)p.cout * (unsigned)p.kpad * 2u;
+
+  char* const Hs = smem;
+  char* const As = smem + 2 * C::HSZ;
+
+  // halo pieces [qa, qb) of job J into halo buffer hb (s2_halo below)
+  auto halo_issue = [&](const S2Job& J, int hb, int qa, int qb) {
+    s2_halo<C::NW>(p, J, Hs + hb * C::HSZ + wave * 1024, hgeo, qa, qb, xbytes, xrow);
+  };
+  // tap column v of job J into column buffer ab (all non-lane terms in the resource base)
+  auto a_issue = [&](const S2Job& J, int v, int ab) {
+    const unsigned o = (unsigned)(J.c0 * p.kpad + v * p.c + 16 * J.k) * 2u;
+    const int nrec = J.valid ? (int)(wbytes - o) : 0;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.w + o), 0, nrec, 0x00020000);
+    char* dst = As + ab * C::WSZ + wave * 1024;
+#pragma unroll
+    for (int q = 0; q < C::WPC; ++q) {
+      // (the offset as a statement of its own: an array element passed straight to the
+      // builtin makes hipcc's host pass drop the kernel's launch stub)
+      const unsigned wo = woff[q];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_s2)(dst + q * C::NW * 1024), 16, wo, 0, 0, 0);
+    }
+  };
+
+  // fragment addresses: A row wc*32*TM + 32 i + r32 (chunk hh, swizzled); B pixel 32 b + r32
+  // of phase row (2 wr + ti, v & 1), shifted by v >> 1, channel group hh
+  int a_off[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wc * 32 * TM + 32 * i + r32;
+    a_off[i] = row * 32 + ((hh ^ ((row >> 3) & 1)) << 4);
+  }
+  const int b_base = (2 * wr * 2 * C::HP + r32) * C::PITCH + hh * 16;
+
+  f32x16 acc[TM][2];
+
+  {
+    const S2Job J0 = tile_job(tile0);
+    halo_issue(J0, 0, 0, C::NHQ);
+    a_issue(J0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  int hb = 0, ab = 0;
+  S2Job J = tile_job(tile0);
+  S2Job J1 = next_job(J);
+  while (J.valid) {
+    if (J.k == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][b][e] = 0.f;
+    }
+    const char* H = Hs + hb * C::HSZ + b_base;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const char* A = As + ab * C::WSZ;
+      // DMA: the next column's weights first, then this column's share of the next job's
+      // halo (the end-of-column wait counts on the halo pieces being the youngest)
+      if (v < 2)
+        a_issue(J, v + 1, ab ^ 1);
+      else
+        a_issue(J1, 0, ab ^ 1);
+      if (v == 0) halo_issue(J1, hb ^ 1, 0, C::H0);
+      if (v == 1) halo_issue(J1, hb ^ 1, C::H0, C::NHQ);
+      const char* Hv = H + ((v & 1) * C::HP + (v >> 1)) * C::PITCH;
+      i32x4 af[3][TM], bf[3][2];
+#pragma unroll
+      for (int ti = 0; ti < 3; ++ti) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[ti][i] = *(const i32x4*)(A + ti * C::TSZ + a_off[i]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[ti][b] = *(const i32x4*)(Hv + (ti * 2 * C::HP + 32 * b) * C::PITCH);
+      }
+#pragma unroll
+      for (int ti = 0; ti < 3; ++ti)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[ti][i]),
+                                                                __builtin_bit_cast(bf16x8, bf[ti][b]), acc[i][b], 0, 0,
+                                                                0);
+      // end of the column: the next column's weights (and after column 2 the next job's halo)
+      // have landed -- this column's halo share may stay in flight -- and every wave's reads
+      // of this column's buffers are done (lgkmcnt 0), so they may be refilled after the barrier
+      if (v == 0)
+        DVIE_S2_VMCNT_LGKM0(C::H0);
+      else if (v == 1)
+        DVIE_S2_VMCNT_LGKM0(C::NHQ - C::H0);
+      else
+        DVIE_S2_VMCNT_LGKM0(0);
+      __builtin_amdgcn_s_barrier();
+      ab ^= 1;
+    }
+    hb ^= 1;
+
+    if (J.k + 1 == nchunks) {
+      // ---- epilogue from the accumulators: permlane32_swap pairs the half-waves so that each
+      // lane owns 8 consecutive channels of one pixel ----
+      const int oy = J.y0 + wr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          float v8[2][8];
+#pragma unroll
+          for (int P = 0; P < 2; ++P)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][b][8 * P + e]),
+                                                               __float_as_uint(acc[i][b][8 * P + 4 + e]), false, false);
+              v8[P][e] = __uint_as_float(sw[0]);
+              v8[P][4 + e] = __uint_as_float(sw[1]);
+            }
+          const int ox = J.x0 + 32 * b + r32;
+          if (oy >= p.oh || ox >= p.ow) continue;
+          const long long pix = ((long long)J.n * p.yh + oy) * p.yw + ox;
+#pragma unroll
+          for (int P = 0; P < 2; ++P) {
+            const int co = J.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh;
+            if (co >= p.cout) continue;
+            float* w = v8[P];
+            if (p.bias) {
+              const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[e] += b0[e];
+                w[4 + e] += b1[e];
+              }
+            }
+            if (EPI & 1) {
+              const i32x4 tr = *(const i32x4*)((const bf16_t*)p.res + pix * p.res_ld + co);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                w[2 * e] += __uint_as_float(((uint32_t)tr[e]) << 16);
+                w[2 * e + 1] += __uint_as_float(((uint32_t)tr[e]) & 0xffff0000u);
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = act_fwd(w[e], p.act, p.alpha);
+            i32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (int)s2_pack(w[2 * e], w[2 * e + 1]);
+            *(i32x4*)((bf16_t*)p.y + pix * p.y_ld + co) = o;
+          }
+        }
+    }
+    J = J1;
+    J1 = next_job(J1);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+template <int TM>
+static void launch_s2(const dvie_conv_desc& p, hipStream_t s) {
+  const int n_ct = (p.cout + S2<TM>::BC - 1) / S2<TM>::BC;
+  const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + S2<TM>::PR - 1) / S2<TM>::PR;
+  const int n_tiles = n_ct * tiles_x * tiles_y * p.n;
+  const int grid = n_tiles > 256 ? 256 : n_tiles;
+  if (p.res)
+    DVIE_LAUNCH((conv_s2_kernel<TM, 1>), dim3(grid), dim3(512), 0, s, p, n_ct, n_tiles, tiles_x, tiles_y);
+  else
+    DVIE_LAUNCH((conv_s2_kernel<TM, 0>), dim3(grid), dim3(512), 0, s, p, n_ct, n_tiles, tiles_x, tiles_y);
+}
+
+// DVIE_CONV_S2=0: stride-2 convs on the per-tap implicit GEMM (A/B runs); read per launch
+static bool s2_on() {
+  const char* e = getenv("DVIE_CONV_S2");
+  return !(e && *e == '0');
+}
+
+// stride-2 3x3 zero-padded forward conv, bf16 output, identity output placement; true when
+// the phase-split halo kernel took the launch
+bool conv_s2_launch(const dvie_conv_desc& p, hipStream_t s) {
+  if (!s2_on() || p.dtype != DVIE_BF16 || p.out_f32 || p.beta || p.dact) return false;
+  if (p.sy != 2 || p.sx != 2 || p.th != 3 || p.tw != 3 || p.dy0 != -1 || p.dx0 != -1 || p.ddy != 1 || p.ddx != 1)
+    return false;
+  if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) return false;
+  if (p.c % 16 != 0 || p.cout % 8 != 0 || p.kpad < 9 * p.c) return false;
+  if ((p.res && p.res_ld % 8 != 0) || p.y_ld % 8 != 0 || p.x_ld % 8 != 0) return false;
+  const unsigned long long pix = (unsigned long long)p.n * p.ih * p.iw;
+  if (((pix - 1) * (unsigned long long)p.x_ld + (unsigned long long)p.c) * 2ull >= 0xFFFFFF00ull) return false;
+  if ((unsigned long long)p.cout * p.kpad * 2ull >= 0xFFFFFF00ull) return false;
+  // expected output grid of a pad-1 stride-2 3x3 conv
+  if (p.oh != (p.ih - 1) / 2 + 1 || p.ow != (p.iw - 1) / 2 + 1) return false;
+  const long long nt = (long long)p.n * ((p.oh + 3) / 4) * ((p.ow + 63) / 64) * ((p.cout + 63) / 64);
+  if (nt >= (1LL << 30)) return false;
+  if (p.cout <= 64)
+    launch_s2<1>(p, s);
+  else if (p.cout <= 128)
+    launch_s2<2>(p, s);
+  else
+    launch_s2<4>(p, s);
+  return true;
+}
+
+}  // namespace dvie
