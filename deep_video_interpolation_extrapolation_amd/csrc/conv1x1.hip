@@ -730,6 +730,7 @@ bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s) {
     case 116: one ? launch_1x1<4, 1, 64, 4, 2, 2>(p, s) : launch_1x1<4, 2, 64, 4, 2, 2>(p, s); break;
     case 118: one ? launch_1x1<2, 1, 64, 4, 2, 2>(p, s) : launch_1x1<2, 3, 64, 4, 2, 2>(p, s); break;
     case 119: one ? launch_1x1<4, 1, 64, 4, 2, 2>(p, s) : launch_1x1<4, 4, 32, 4, 2, 2>(p, s); break;
+    case 120: one ? launch_1x1<4, 1, 64, 4, 2, 2>(p, s) : launch_1x1<4, 5, 32, 4, 2, 2>(p, s); break;
     default: return false;
   }
   return true;

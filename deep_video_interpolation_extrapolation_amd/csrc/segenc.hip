@@ -257,6 +257,19 @@ __device__ __forceinline__ bf16x8 hb_tr_pair_se(const char* p0, const char* p1) 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// t + the sum of a fragment's 8 bf16 values, in fp32 (four v_dot2c_f32_bf16 against (1, 1))
+__device__ __forceinline__ float sum8_bf16_se(const bf16x8 v, float t) {
+  typedef __bf16 bf16x2_se __attribute__((ext_vector_type(2)));
+  const i32x4 u = __builtin_bit_cast(i32x4, v);
+  const bf16x2_se one = __builtin_bit_cast(bf16x2_se, 0x3F803F80);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int w = u[e];
+    t = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_se, w), one, t, false);
+  }
+  return t;
+}
+
 struct SbCfg {
   static constexpr int NW = 8, R = 4, TW = 64;
   static constexpr int DO_W = TW + 4, DO_H = R + 4;  // origin (-2, -2)
@@ -267,8 +280,8 @@ struct SbCfg {
   static constexpr int W4_PITCH = 5 * 32 + 16, W2_PITCH = 18 * 32 + 16;
   static constexpr int O_DO = 0, O_E2 = O_DO + DO_PC * 1024, O_E1 = O_E2 + E_PC * 1024, O_IN = O_E1 + E_PC * 1024;
   static constexpr int O_D2 = O_IN + IN_PC * 1024, O_D1 = O_D2 + E_H * E_W * 64, O_W4 = O_D1 + R * TW * 64;
-  static constexpr int O_W2 = O_W4 + 32 * W4_PITCH, O_RED = O_W2 + 32 * W2_PITCH;
-  static constexpr int SMEM = O_RED + 8 * 72 * 4;
+  static constexpr int O_W2 = O_W4 + 32 * W4_PITCH, O_END = O_W2 + 32 * W2_PITCH;
+  static constexpr int SMEM = O_END;
   static constexpr int PCS = DO_PC + 2 * E_PC + IN_PC;  // DMA pieces per tile
   static constexpr int PQ = (PCS + NW - 1) / NW;
 };
@@ -339,36 +352,59 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-  float bsum = 0.f;  // bias partial: thread tid < 504 owns channel tid % 72, pixels tid / 72 + 7 k
+  float bsum = 0.f;  // bias partial of the A rows (waves 0 / 3 / 6: dout / d_e2 / d_e1)
 
-  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+  // The next tile's four images are loaded into registers (10 x 16 B per lane) while this
+  // tile's three phases run, and written to LDS at the next tile's start: the global-memory
+  // latency of a tile's operands hides behind the previous tile's MFMAs (there is no room for a
+  // second set of LDS images).
+  i32x4 stg[C::PQ];
+  auto tile_pos = [&](int t, int& n, int& y0, int& x0) {
     int tt = t;
-    const int x0 = (tt % tiles_x) * C::TW;
+    x0 = (tt % tiles_x) * C::TW;
     tt /= tiles_x;
-    const int y0 = (tt % tiles_y) * C::R;
-    const int n = tt / tiles_y;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+    y0 = (tt % tiles_y) * C::R;
+    n = tt / tiles_y;
+  };
+  auto load_tile = [&](int t) {
+    int n, y0, x0;
+    tile_pos(t, n, y0, x0);
 #pragma unroll
     for (int q = 0; q < C::PQ; ++q) {
       const int pc = wave + NW * q;
       if (pc >= C::PCS) continue;  // (wave-uniform)
       const int v = geo[q];
-      // (image from the piece index: the LDS destination must be wave-uniform)
       const int img = pc < C::DO_PC ? 0 : pc < C::DO_PC + C::E_PC ? 1 : pc < C::DO_PC + 2 * C::E_PC ? 2 : 3;
       const int org = img == 0 ? 2 : 1;
       const int iy = y0 - org + ((v >> 20) & 0xFF), ix = x0 - org + ((v >> 8) & 0xFFF);
       const bool ok = v >= 0 && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
       const unsigned o = ok ? (unsigned)((n * p.h + iy) * p.w + ix) * rows[img] + (unsigned)(v & 15) * 16u : OOB;
-      int dst = img == 0 ? C::O_DO + pc * 1024
-                         : img == 1 ? C::O_E2 + (pc - C::DO_PC) * 1024
-                                    : img == 2 ? C::O_E1 + (pc - C::DO_PC - C::E_PC) * 1024
-                                               : C::O_IN + (pc - C::DO_PC - 2 * C::E_PC) * 1024;
       __amdgpu_buffer_rsrc_t r = img == 0 ? rs[0] : img == 1 ? rs[1] : img == 2 ? rs[2] : rs[3];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_se)(smem + dst), 16, o, 0, 0, 0);
+      stg[q] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
     }
-    __builtin_amdgcn_s_waitcnt(0);
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int q = 0; q < C::PQ; ++q) {
+      const int pc = wave + NW * q;
+      if (pc >= C::PCS) continue;
+      const int img = pc < C::DO_PC ? 0 : pc < C::DO_PC + C::E_PC ? 1 : pc < C::DO_PC + 2 * C::E_PC ? 2 : 3;
+      const int dst = img == 0 ? C::O_DO + pc * 1024
+                               : img == 1 ? C::O_E2 + (pc - C::DO_PC) * 1024
+                                          : img == 2 ? C::O_E1 + (pc - C::DO_PC - C::E_PC) * 1024
+                                                     : C::O_IN + (pc - C::DO_PC - 2 * C::E_PC) * 1024;
+      *(i32x4*)(smem + dst + lane * 16) = stg[q];
+    }
+  };
+  if ((int)blockIdx.x < n_tiles) load_tile(blockIdx.x);
+
+  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    int n, y0, x0;
+    tile_pos(t, n, y0, x0);
+    __syncthreads();  // the previous tile's reads of the images are done
+    store_tile();
     __syncthreads();
+    if (t + (int)gridDim.x < n_tiles) load_tile(t + gridDim.x);
 
     // ---- phase 1: d_e2 on the 6 x 66 region = ELU'(e2) * conv4^T(dout) ----
     for (int blk = wave; blk < (C::E_H * C::E_W + 31) / 32; blk += NW) {
@@ -499,28 +535,9 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
         }
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, hb_tr_pair_se(b0, b1), acc[j], 0, 0, 0);
       }
-    }
-    // ---- bias column sums (dout 8, d_e2 32, d_e1 32 channels over the tile) ----
-    if (tid < 504) {
-      const int ch = tid % 72, part = tid / 72;
-      for (int px = part; px < 256; px += 7) {
-        const int rr = px >> 6, cc = px & 63;
-        const char* a;
-        int c;
-        if (ch < 8) {
-          a = smem + C::O_DO + ((rr + 2) * C::DO_W + cc + 2) * 16;
-          c = ch;
-        } else if (ch < 40) {
-          c = ch - 8;
-          a = smem + C::O_D2 + sw64((rr + 1) * C::E_W + cc + 1, c >> 3);
-          c &= 7;
-        } else {
-          c = ch - 40;
-          a = smem + C::O_D1 + sw64(px, c >> 3);
-          c &= 7;
-        }
-        bsum += bf2f(*(const bf16_t*)(a + c * 2));
-      }
+      // bias column sums from the A fragment: lane l holds 8 pixels of row l % 32 (the first
+      // wave of each gemm sums; every wave does the VALU work, no branch splits the k-step)
+      bsum = sum8_bf16_se(av, bsum);
     }
   }
 
@@ -543,20 +560,12 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
         }
     }
   }
-  float* red = (float*)(smem + C::O_RED);
-  __syncthreads();
-  if (tid < 504) red[tid] = bsum;
-  __syncthreads();
-  if (tid < 72) {
-    float s = 0.f;
-    for (int k = 0; k < 7; ++k) s += red[k * 72 + tid];
-    if (tid < 8)
-      p.db4[slab * 8 + tid] = s;
-    else if (tid < 40)
-      p.db2[slab * 32 + tid - 8] = s;
-    else
-      p.db0[slab * 32 + tid - 40] = s;
-  }
+  // bias partials: lanes l and l + 32 hold the two 8-pixel halves of row l % 32 (dout's
+  // rows 8..31 are copies of rows 0..7)
+  const float bt = bsum + __shfl_xor(bsum, 32, 64);
+  if (wave == 0 && lane < 8) p.db4[slab * 8 + lane] = bt;
+  if (wave == 3 && lane < 32) p.db2[slab * 32 + lane] = bt;
+  if (wave == 6 && lane < 32) p.db0[slab * 32 + lane] = bt;
 }
 
 }  // namespace dvie

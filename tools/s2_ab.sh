@@ -15,6 +15,6 @@ for e in "${envs[@]}"; do
   i=$((i+1))
   ( export $e; timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $out/r$i -o k -- python3 tools/conv_micro.py "$@" > $out/r$i.log 2>&1 ) || { echo "run $i ($e) failed"; tail -5 $out/r$i.log; exit 1; }
   f=$(find $out/r$i -name '*kernel_stats.csv')
-  echo "== $e"; grep -E "conv_s2|conv_igemm|conv_dg|wgrad" $f | cut -d, -f1-4 || true
+  echo "== $e"; grep -E "conv_s2|conv_igemm|conv1x1|wgrad" $f | cut -d, -f1-4 || true
   rm -f $out/r$i/*/*kernel_trace.csv
 done
