@@ -131,16 +131,31 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
   const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.in, 0, (int)((npx - 1) * p.in_ld * 2ull + 48ull), 0x00020000);
 
-  const int G = gridDim.x;
-  for (int t = blockIdx.x; t < n_tiles; t += G) {
+  // biases in registers (a lane's epilogue channels: 16 P + 8 hh .. +7)
+  float bb0[2][8], bb2[2][8], bb4[8];
+#pragma unroll
+  for (int P = 0; P < 2; ++P)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bb0[P][e] = p.b0[16 * P + 8 * hh + e];
+      bb2[P][e] = p.b2[16 * P + 8 * hh + e];
+    }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bb4[e] = p.b4[e];
+
+  // The next tile's input halo is loaded into registers while this tile's three stages run
+  // and written to LDS at the next tile's start (its global latency hides behind the MFMAs).
+  i32x4 stg[IQ];
+  auto tile_pos = [&](int t, int& n, int& y0, int& x0) {
     int tt = t;
-    const int x0 = (tt % tiles_x) * C::TW;
+    x0 = (tt % tiles_x) * C::TW;
     tt /= tiles_x;
-    const int y0 = (tt % tiles_y) * C::R;
-    const int n = tt / tiles_y;
-    // previous tile's readers are done with every image (and the weights have landed)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+    y0 = (tt % tiles_y) * C::R;
+    n = tt / tiles_y;
+  };
+  auto load_tile = [&](int t) {
+    int n, y0, x0;
+    tile_pos(t, n, y0, x0);
 #pragma unroll
     for (int q = 0; q < IQ; ++q) {
       const int pc = wave + NW * q;
@@ -149,10 +164,23 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
       const int iy = y0 - 3 + ((v >> 16) & 0xFF), ix = x0 - 3 + ((v >> 4) & 0xFFF);
       const bool ok = v >= 0 && (unsigned)iy < (unsigned)p.h && (unsigned)ix < (unsigned)p.w;
       const unsigned o = ok ? (unsigned)((n * p.h + iy) * p.w + ix) * irow + (unsigned)(v & 15) * 16u : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_ptr_se)(smem + C::O_IN + pc * 1024), 16, o, 0, 0, 0);
+      stg[q] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, o, 0, 0));
     }
-    __builtin_amdgcn_s_waitcnt(0);
+  };
+  const int G = gridDim.x;
+  if ((int)blockIdx.x < n_tiles) load_tile(blockIdx.x);
+  for (int t = blockIdx.x; t < n_tiles; t += G) {
+    int n, y0, x0;
+    tile_pos(t, n, y0, x0);
+    // previous tile's readers are done with every image (and the weights have landed)
     __syncthreads();
+#pragma unroll
+    for (int q = 0; q < IQ; ++q) {
+      const int pc = wave + NW * q;
+      if (pc < C::IN_PC) *(i32x4*)(smem + C::O_IN + pc * 1024 + lane * 16) = stg[q];
+    }
+    __syncthreads();
+    if (t + G < n_tiles) load_tile(t + G);
 
     // ---- e1 on the 8 x 68 region at (y0 - 2, x0 - 2) ----
     se_stage<C::KS0, 3, C::E1_W, C::IN_PITCH, C::W0_PITCH>(
@@ -166,8 +194,8 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
             i32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float a = in ? act_fwd(v[P][2 * e] + p.b0[co + 2 * e], DVIE_ACT_ELU, 0.f) : 0.f;
-              const float b = in ? act_fwd(v[P][2 * e + 1] + p.b0[co + 2 * e + 1], DVIE_ACT_ELU, 0.f) : 0.f;
+              const float a = in ? act_fwd(v[P][2 * e] + bb0[P][2 * e], DVIE_ACT_ELU, 0.f) : 0.f;
+              const float b = in ? act_fwd(v[P][2 * e + 1] + bb0[P][2 * e + 1], DVIE_ACT_ELU, 0.f) : 0.f;
               o[e] = (int)se_pack(a, b);
             }
             *(i32x4*)(smem + C::O_E1 + (r * C::E1_W + c) * C::E_PITCH + co * 2) = o;
@@ -187,8 +215,8 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
             i32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float a = in ? act_fwd(v[P][2 * e] + p.b2[co + 2 * e], DVIE_ACT_ELU, 0.f) : 0.f;
-              const float b = in ? act_fwd(v[P][2 * e + 1] + p.b2[co + 2 * e + 1], DVIE_ACT_ELU, 0.f) : 0.f;
+              const float a = in ? act_fwd(v[P][2 * e] + bb2[P][2 * e], DVIE_ACT_ELU, 0.f) : 0.f;
+              const float b = in ? act_fwd(v[P][2 * e + 1] + bb2[P][2 * e + 1], DVIE_ACT_ELU, 0.f) : 0.f;
               o[e] = (int)se_pack(a, b);
             }
             *(i32x4*)(smem + C::O_E2 + (r * C::E2_W + c) * C::E_PITCH + co * 2) = o;
@@ -203,7 +231,7 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
           if (hh || gy >= p.h || gx >= p.w) return;  // channels 0..7 = pair 0, lane half 0
           i32x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (int)se_pack(v[0][2 * e] + p.b4[2 * e], v[0][2 * e + 1] + p.b4[2 * e + 1]);
+          for (int e = 0; e < 4; ++e) o[e] = (int)se_pack(v[0][2 * e] + bb4[2 * e], v[0][2 * e + 1] + bb4[2 * e + 1]);
           *(i32x4*)((bf16_t*)p.out + ((long long)(n * p.h + gy) * p.w + gx) * p.out_ld) = o;
         });
   }
@@ -454,18 +482,25 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
     {
       const int blk = wave;  // 8 blocks of 32 pixels
       const int q = blk * 32 + r32, rr = q >> 6, cc = q & 63;
-      f32x16 a1;
+      // (the K = 288 chain split over two accumulators: two independent MFMA chains)
+      f32x16 a1, a1b;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+      for (int e = 0; e < 16; ++e) a1[e] = a1b[e] = 0.f;
 #pragma unroll
       for (int s = 0; s < 18; ++s) {
         const i32x4 a = *(const i32x4*)(smem + C::O_W2 + r32 * C::W2_PITCH + hh * 16 + s * 32);
         const int kc = 2 * s + hh, tp = kc >> 2, ck = kc & 3;
         const int pe = (rr + tp / 3) * C::E_W + cc + tp % 3;
         const i32x4 b = *(const i32x4*)(smem + C::O_D2 + sw64(pe, ck));
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1, 0,
-                                                     0, 0);
+        if (s & 1)
+          a1b = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1b,
+                                                        0, 0, 0);
+        else
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1,
+                                                       0, 0, 0);
       }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a1[e] += a1b[e];
       const int gy = y0 + rr, gx = x0 + cc;
       const bool in = gy < p.h && gx < p.w;
       const int pe = (rr + 1) * C::E_W + cc + 1;
