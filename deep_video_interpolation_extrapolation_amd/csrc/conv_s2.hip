@@ -18,8 +18,8 @@
 // One vmcnt wait + barrier per column; the wait leaves the two younger weight columns and the
 // halo shares that are not yet needed in flight.
 //   8 MFMA waves = 2 (output-channel halves of 32 TM) x 4 (output rows); a wave owns 32 TM
-// channels x 1 row x 64 pixels (2 TM accumulators of 32 x 32).  For TM <= 2 two more waves
-// issue all the LDS-DMA (the MFMA waves then never stall behind the address unit).  LDS:
+// channels x 1 row x 64 pixels (2 TM accumulators of 32 x 32).  Two more waves
+// issue all the LDS-DMA (TM = 2; the MFMA waves then never stall behind the address unit).  LDS:
 // 2 x 40 KB halo + 3 column buffers (8 / 16 / 24 KB for TM = 1 / 2 / 4): one workgroup per
 // CU, persistent over an XCD-contiguous tile range.  Epilogue from registers: bias, residual
 // (EPI bit 1), activation.
@@ -339,11 +339,13 @@ __global__ __launch_bounds__(64 * (8 + DW)) void conv_s2_kernel(const dvie_conv_
   __builtin_amdgcn_s_waitcnt(0);
 }
 
-// TM <= 2: two dedicated DMA waves beside the eight MFMA waves (8x256x512 256->128:
-// 276 -> 262 us, tools/s2_ab.sh); TM = 4 has no registers for a third wave per SIMD
+// TM = 2: two dedicated DMA waves beside the eight MFMA waves (8x256x512 256->128:
+// 276 -> 262 us, tools/s2_ab.sh; 8x128x256 64->64, TM = 1: 21.9 us without, 23.2 with them);
+// TM = 4 has no registers for a third wave per SIMD.  (Hoisting every fragment read of a
+// column ahead of its MFMAs with a scheduling barrier: 262 -> 287 us, not kept.)
 template <int TM>
 static void launch_s2(const dvie_conv_desc& p, hipStream_t s) {
-  constexpr int DW = TM <= 2 ? 2 : 0;
+  constexpr int DW = TM == 2 ? 2 : 0;
   typedef S2<TM, DW> C;
   const int n_ct = (p.cout + C::BC - 1) / C::BC;
   const int tiles_x = (p.ow + 63) / 64, tiles_y = (p.oh + C::PR - 1) / C::PR;
