@@ -591,6 +591,237 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_persist_kernel(const d
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+// Ring form for the wide multi-K-step layers without epilogue operands (the heads' 448 -> 896
+// forward): 256 x 256 tiles, 64-channel K-steps, persistent over the workgroup's tiles.  The
+// LDS is a ring of five 32-KB slots, each holding ONE operand of one K-step (the x rows or the
+// weight rows, 128-B rows as above); "half-stage" h = operand h & 1 of job h >> 1 (job = tile,
+// K-step) lives in slot h % 5.  At job j the slots of job j - 1 are refilled with half-stages
+// 2j + 3 and 2j + 4, so three half-stages (96 KB) are in flight after the issue and one at the
+// wait -- against the two-stage form's one 64-KB stage, issued in one burst and drained at
+// every K-step.  Each wave issues 4 pieces per half-stage (uniform, so the waits are counted).
+// The bias is loaded into the accumulators when a tile starts (before that job's DMA issue, so
+// waiting for it drains nothing); the epilogue (activation, bf16 stores, general output
+// placement) reads no memory.
+// AB: timing-only ablations (instantiated in -DDVIE_TIMING_DBG builds only; DVIE_1X1_DBG):
+// 1 no stores, 2 no MFMAs, 4 no DMA after the prologue
+template <int TMC, int NWP, int MI, int NWC, int ACT, int AB = 0>
+__global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_ring_kernel(const dvie_conv_desc p, int n_ct, int n_tiles) {
+  constexpr int dbg = AB;
+  typedef G1Cfg<TMC, 2, 64, NWP, MI, NWC> C;
+  constexpr int NW = C::NW, SL = 32768, NSLOT = 5, PPH = 4;  // pieces per wave per half-stage
+  static_assert(C::XSZ == SL && C::WSZ == SL && C::XQ == PPH && C::WQ == PPH && C::BC / C::RPP == NW * PPH,
+                "ring slot = one operand of one K-step, 4 pieces per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned OOB = 0xFFFFFFF0u;
+
+  const int G = gridDim.x;
+  const int g = blockIdx.x & 7, i8 = blockIdx.x >> 3;
+  const int q8 = G >> 3, r8 = G & 7;
+  const int b = (g < r8 ? g * (q8 + 1) : r8 * (q8 + 1) + (g - r8) * q8) + i8;
+  const int npix = p.n * p.oh * p.ow;
+  const int nk = (p.c + 63) / 64;
+  const int my_tiles = b < n_tiles ? (n_tiles - 1 - b) / G + 1 : 0;
+  const int njobs = my_tiles * nk;
+  if (njobs == 0) return;
+
+  const int lrow = lane / C::NCH, lch = lane % C::NCH;
+  const unsigned long long xbytes =
+      ((unsigned long long)p.n * p.ih * p.iw - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+  const unsigned wbytes = (unsigned)p.cout * (unsigned)p.kpad * 2u;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, (int)wbytes, 0x00020000);
+  const unsigned long long ybytes =
+      ((unsigned long long)p.n * p.yh * p.yw - 1) * (unsigned long long)p.y_ld * 2ull + (unsigned long long)p.cout * 2ull;
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.y, 0, (int)ybytes, 0x00020000);
+  // (no bias: a zero-length range, every load returns zeros)
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.cout * 4 : 0, 0x00020000);
+
+  // per-lane DMA geometry, once: piece q row (the same for both operands) and its byte offset
+  // within a row block (channel chunk swizzled); the per-issue part is wave-uniform
+  int prow[PPH];
+  unsigned xoff[PPH], woff[PPH], chk[PPH];
+#pragma unroll
+  for (int q = 0; q < PPH; ++q) {
+    const int row = (wave + NW * q) * C::RPP + lrow;
+    const int cs = lch ^ C::swz(row);
+    prow[q] = row;
+    chk[q] = (unsigned)cs * 8u;
+    xoff[q] = (unsigned)row * (unsigned)p.x_ld * 2u + (unsigned)cs * 16u;
+    woff[q] = (unsigned)row * (unsigned)p.kpad * 2u + (unsigned)cs * 16u;
+  }
+  // a cursor over this workgroup's jobs (tile i, K-step k), advanced one job at a time
+  struct Cur {
+    int i, k, c0, p0;
+  };
+  auto cur_at = [&](int jj) {  // (divisions: a few times per workgroup)
+    Cur c;
+    c.i = jj / nk;
+    c.k = jj - c.i * nk;
+    const int T = b + c.i * G;
+    c.c0 = (T % n_ct) * C::BC;
+    c.p0 = (T / n_ct) * C::BP;
+    return c;
+  };
+  auto cur_next = [&](Cur c) {
+    if (++c.k == nk) {
+      c.k = 0;
+      ++c.i;
+      const int T = b + c.i * G;
+      c.c0 = (T % n_ct) * C::BC;
+      c.p0 = (T / n_ct) * C::BP;
+    }
+    return c;
+  };
+  // operand wop of job (cursor c, live) into slot sl; a dead job (past the last) issues zero
+  // pieces, so every wave's count per half-stage stays 4
+  auto issue = [&](const Cur& c, bool live, int wop, int sl) {
+    char* dst = smem + sl * SL + wave * 1024;
+    const int cvalid = live ? p.c - 64 * c.k : 0;
+    const int lim = live ? (wop ? p.cout - c.c0 : npix - c.p0) : 0;
+    const unsigned base = wop ? (unsigned)c.c0 * (unsigned)p.kpad * 2u + 128u * (unsigned)c.k
+                              : (unsigned)c.p0 * (unsigned)p.x_ld * 2u + 128u * (unsigned)c.k;
+#pragma unroll
+    for (int q = 0; q < PPH; ++q) {
+      const bool ok = prow[q] < lim && (cvalid >= 64 || (int)chk[q] < cvalid);
+      const unsigned o = ok ? base + (wop ? woff[q] : xoff[q]) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wop ? rw : rx, (lds_ptr_1x1)(dst + q * NW * 1024), 16, o, 0, 0, 0);
+    }
+  };
+
+  const int wp = wave % NWP, wc = wave / NWP;
+  int xf[C::NSL], wf[C::NSL];
+#pragma unroll
+  for (int sl = 0; sl < C::NSL; ++sl) {
+    const int pr = wp * 32 * MI + r32;
+    xf[sl] = pr * C::RB + (((2 * sl + hh) ^ C::swz(pr)) << 4);
+    wf[sl] = (wc * 32 * TMC + r32) * C::RB + (((2 * sl + hh) ^ C::swz(r32)) << 4);
+  }
+  // the bias of a lane in accumulator layout: rows 8 u + 4 hh + 0..3 of 32-channel block j
+  const int bco = wc * 32 * TMC + 4 * hh;
+
+  f32x16 acc[MI][TMC];
+  // prologue: half-stages 0 (x of job 0), 1 (w of job 0), 2 (x of job 1)
+  Cur cj = cur_at(0);                // the job being computed
+  Cur cw = cur_next(cj);             // the job whose weights issue next (jj + 1)
+  Cur cx = cur_next(cw);             // the job whose x rows issue next (jj + 2)
+  issue(cj, true, 0, 0);
+  issue(cj, true, 1, 1);
+  issue(cw, 1 < njobs, 0, 2);
+  int s0 = 0;  // slot of job jj's x rows (2 jj mod 5); its weights are in slot s0 + 1 mod 5
+  int jj = 0;
+  // one job: the counted wait + barrier, the refill of job jj - 1's slots (the weights of job
+  // jj + 1 = half-stage 2 jj + 3, the x rows of job jj + 2 = 2 jj + 4), the bias at a tile's
+  // first job (loaded before the refill, so waiting for it drains nothing), the MFMAs
+  auto job = [&](bool first, bool after_epi) {
+    // half-stages <= 2 jj + 1 have landed (this wave's pieces by the count, the others' by the
+    // barrier); only 2 jj + 2 -- plus the previous tile's epilogue stores -- may be in flight;
+    // every wave's reads of job jj - 1's slots are done (lgkmcnt 0)
+    if (after_epi)
+      DVIE_VMCNT1(PPH + 2 * MI * TMC);
+    else
+      DVIE_VMCNT1(PPH);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    f32x4 bi[TMC][4];
+    if (first) {
+#pragma unroll
+      for (int j = 0; j < TMC; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int co = cj.c0 + bco + 32 * j + 8 * u;
+          // (a buffer load with an out-of-range offset past cout: zeros, no branch)
+          bi[j][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, co < p.cout ? (unsigned)co * 4u : OOB, 0, 0));
+        }
+    }
+    if (!(dbg & 4)) {
+      const int sw = s0 + 3 >= NSLOT ? s0 + 3 - NSLOT : s0 + 3, sx = s0 + 4 >= NSLOT ? s0 + 4 - NSLOT : s0 + 4;
+      issue(cw, jj + 1 < njobs, 1, sw);
+      issue(cx, jj + 2 < njobs, 0, sx);
+    }
+    if (first) {
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int j = 0; j < TMC; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[ii][j][e] = bi[j][e >> 2][e & 3];
+    }
+    const char* X = smem + s0 * SL;
+    const char* W = smem + (s0 + 1 >= NSLOT ? s0 + 1 - NSLOT : s0 + 1) * SL;
+#pragma unroll
+    for (int sl = 0; sl < C::NSL; ++sl) {
+      if (dbg & 2) break;
+      i32x4 bq[MI], a[TMC];
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii) bq[ii] = *(const i32x4*)(X + xf[sl] + ii * 32 * C::RB);
+#pragma unroll
+      for (int j = 0; j < TMC; ++j) a[j] = *(const i32x4*)(W + wf[sl] + j * 32 * C::RB);
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int j = 0; j < TMC; ++j)
+          acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[j]),
+                                                               __builtin_bit_cast(bf16x8, bq[ii]), acc[ii][j], 0, 0, 0);
+    }
+    s0 = s0 + 2 >= NSLOT ? s0 + 2 - NSLOT : s0 + 2;
+    cj = cw;
+    cw = cx;
+    cx = cur_next(cx);
+    ++jj;
+  };
+  for (int it = 0; it < my_tiles; ++it) {
+    const int c0 = cj.c0, p0 = cj.p0;
+    // the tile's first K-step peeled off its loop: the accumulators start from the bias there
+    // and stay in place through the loop (no branch merges them)
+    job(true, it > 0);
+    for (int k = 1; k < nk; ++k) job(false, false);
+
+    // ---- epilogue of tile T: activation, bf16 stores (2 MI TMC per lane), output placement
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii) {
+      const int pix0 = p0 + wp * 32 * MI + 32 * ii + r32;
+      const bool pix_ok = pix0 < npix;
+      const int pix = pix_ok ? pix0 : npix - 1;
+      long long yp = pix;
+      if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) {
+        const int hw = p.oh * p.ow;
+        const int n = pix / hw, r = pix - n * hw;
+        const int oy = r / p.ow, ox = r - oy * p.ow;
+        yp = ((long long)n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+      }
+#pragma unroll
+      for (int j = 0; j < TMC; ++j)
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          float w[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[ii][j][8 * P + e]),
+                                                             __float_as_uint(acc[ii][j][8 * P + 4 + e]), false, false);
+            w[e] = __uint_as_float(sw[0]);
+            w[4 + e] = __uint_as_float(sw[1]);
+          }
+          if (ACT == DVIE_ACT_LRELU) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = fmaxf(w[e], w[e] * p.alpha);  // (0 <= alpha <= 1: launch)
+          }
+          i32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (int)pk_bf16(w[2 * e], w[2 * e + 1]);
+          const int co = c0 + wc * 32 * TMC + 32 * j + 16 * P + 8 * hh;
+          // (a buffer store that every wave issues, out-of-range lanes aimed past the buffer's
+          // range and dropped: the per-wave store count the next wait counts on is uniform)
+          const unsigned yo = (pix_ok && co < p.cout && !(dbg & 1)) ? (unsigned)((yp * p.y_ld + co) * 2) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), ry, yo, 0, 0);
+        }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 // operand sets instantiated per tile shape: single K-step, at most 4 accumulators per wave
 // (a single prefetched operand on the 8-accumulator 64->256 tile measured no gain)
 template <int V, int NS, int MT>
@@ -613,6 +844,12 @@ static int dbg_env() {
 #else
   return 0;
 #endif
+}
+
+// DVIE_1X1_RING=0: the wide multi-K-step layers on the two-stage kernel (A/B runs); read per launch
+static bool ring_env_on() {
+  const char* e = getenv("DVIE_1X1_RING");
+  return !(e && *e == '0');
 }
 
 // DVIE_1X1_CE=0: the MFMA-layout epilogue stores for the single-K-step wide tiles (A/B runs);
@@ -638,6 +875,33 @@ static void launch_1x1(const dvie_conv_desc& p, hipStream_t s) {
   if (p.out_f32) {
     DVIE_LAUNCH((conv1x1_kernel<TMC, NS, KC, NWP, MI, NWC, true>), dim3(n_tiles), dim3(64 * NW), 0, s, p, n_ct, n_tiles, dbg_env());
     return;
+  }
+  if constexpr (NS == 2 && KC == 64 && TMC == 4 && NWP == 4 && MI == 2 && NWC == 2) {
+    // the wide multi-K-step layers without epilogue operands: the five-slot operand ring
+    const unsigned long long span = ((unsigned long long)p.n * p.yh * p.yw - 1) * (unsigned long long)p.y_ld * 2ull +
+                                    (unsigned long long)p.cout * 2ull;
+    const unsigned long long xspan = ((unsigned long long)npix - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
+    if (ring_env_on() && p.c > KC && n_tiles > 256 && !p.res && !p.beta && !p.dact && span < 0xFFFFFF00ull &&
+        xspan < 0xFFFFFF00ull && p.ih == p.oh && p.iw == p.ow &&
+        (p.act == DVIE_ACT_NONE || (p.act == DVIE_ACT_LRELU && p.alpha >= 0.f && p.alpha <= 1.f))) {
+#ifdef DVIE_TIMING_DBG
+      if (p.act == DVIE_ACT_LRELU) switch (dbg_env() & 7) {
+#define DVIE_RING_AB(V)                                                                                                \
+  case V:                                                                                                              \
+    DVIE_LAUNCH((conv1x1_ring_kernel<TMC, NWP, MI, NWC, DVIE_ACT_LRELU, V>), dim3(256), dim3(64 * NW), 0, s, p, n_ct, \
+                n_tiles);                                                                                              \
+    return;
+          DVIE_RING_AB(1) DVIE_RING_AB(2) DVIE_RING_AB(3) DVIE_RING_AB(4) DVIE_RING_AB(5) DVIE_RING_AB(6) DVIE_RING_AB(7)
+#undef DVIE_RING_AB
+          default: break;
+        }
+#endif
+      if (p.act == DVIE_ACT_LRELU)
+        DVIE_LAUNCH((conv1x1_ring_kernel<TMC, NWP, MI, NWC, DVIE_ACT_LRELU>), dim3(256), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
+      else
+        DVIE_LAUNCH((conv1x1_ring_kernel<TMC, NWP, MI, NWC, DVIE_ACT_NONE>), dim3(256), dim3(64 * NW), 0, s, p, n_ct, n_tiles);
+      return;
+    }
   }
   if constexpr (NS >= 2 && NS <= 5 && MI * TMC <= 4) {
     // several K-steps and more tiles than resident workgroups: persistent stage ring
