@@ -99,6 +99,30 @@ __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
   }
 }
 
+// ELU / tanh for the bf16-output kernels: v_exp_f32-based forms, a few instructions each
+// instead of the libm expansions (which, inlined for every output element of an unrolled
+// epilogue, made those kernels 10-14K instructions long).  Accuracy: expm1 within ~2e-7
+// absolute (Taylor below |v| = 1/32), tanh within ~2e-7 absolute (odd Taylor below 1/64) --
+// far inside the bf16 rounding of the stored result.
+__device__ __forceinline__ float elu_bf(float v) {
+  const float t = v > -0.03125f ? v * (1.f + v * (0.5f + v * (1.f / 6.f))) : __expf(v) - 1.f;
+  return v > 0.f ? v : t;
+}
+__device__ __forceinline__ float tanh_bf(float v) {
+  const float a = fabsf(v), e = __expf(-2.f * a);
+  const float t = a < 0.015625f ? a * (1.f - a * a * (1.f / 3.f)) : (1.f - e) * __frcp_rn(1.f + e);
+  return copysignf(t, v);
+}
+__device__ __forceinline__ float act_bf(float v, int act, float alpha) {
+  switch (act) {
+    case DVIE_ACT_LRELU: return v > 0.f ? v : v * alpha;
+    case DVIE_ACT_ELU: return elu_bf(v);
+    case DVIE_ACT_RELU: return v > 0.f ? v : 0.f;
+    case DVIE_ACT_TANH: return tanh_bf(v);
+    default: return v;
+  }
+}
+
 // derivative expressed through the activation OUTPUT z
 __device__ __forceinline__ float act_dz(float z, int act, float alpha) {
   switch (act) {

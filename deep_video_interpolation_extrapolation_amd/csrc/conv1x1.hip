@@ -39,9 +39,9 @@ __device__ __forceinline__ void act1(float* v, int act, float alpha) {
   } else if (act == DVIE_ACT_RELU) {
     for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
   } else if (act == DVIE_ACT_ELU) {
-    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : expm1f(v[k]);
+    for (int k = 0; k < 8; ++k) v[k] = elu_bf(v[k]);  // (bf16-input kernels: common.h)
   } else if (act == DVIE_ACT_TANH) {
-    for (int k = 0; k < 8; ++k) v[k] = tanhf(v[k]);
+    for (int k = 0; k < 8; ++k) v[k] = tanh_bf(v[k]);
   }
 }
 

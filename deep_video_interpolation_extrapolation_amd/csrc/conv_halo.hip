@@ -56,9 +56,9 @@ __device__ __forceinline__ void act_apply(float* v, int n, int act, float alpha)
   } else if (act == DVIE_ACT_RELU) {
     for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
   } else if (act == DVIE_ACT_ELU) {
-    for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : expm1f(v[k]);
+    for (int k = 0; k < n; ++k) v[k] = elu_bf(v[k]);  // (bf16-output kernels only: common.h)
   } else if (act == DVIE_ACT_TANH) {
-    for (int k = 0; k < n; ++k) v[k] = tanhf(v[k]);
+    for (int k = 0; k < n; ++k) v[k] = tanh_bf(v[k]);
   }
 }
 

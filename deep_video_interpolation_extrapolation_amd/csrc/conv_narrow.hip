@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t pk2_bf16(float a, float b) {
 
 __device__ __forceinline__ void narrow_act(float* v, int act, float alpha) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = act_fwd(v[k], act, alpha);
+  for (int k = 0; k < 8; ++k) v[k] = act_bf(v[k], act, alpha);
 }
 
 template <bool OUTF32>

@@ -325,7 +325,7 @@ __global__ __launch_bounds__(64 * (8 + DW)) void conv_s2_kernel(const dvie_conv_
               }
             }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) w[e] = act_fwd(w[e], p.act, p.alpha);
+            for (int e = 0; e < 8; ++e) w[e] = act_bf(w[e], p.act, p.alpha);
             i32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (int)s2_pack(w[2 * e], w[2 * e + 1]);

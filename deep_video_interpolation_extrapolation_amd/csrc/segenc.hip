@@ -194,8 +194,8 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
             i32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float a = in ? act_fwd(v[P][2 * e] + bb0[P][2 * e], DVIE_ACT_ELU, 0.f) : 0.f;
-              const float b = in ? act_fwd(v[P][2 * e + 1] + bb0[P][2 * e + 1], DVIE_ACT_ELU, 0.f) : 0.f;
+              const float a = in ? elu_bf(v[P][2 * e] + bb0[P][2 * e]) : 0.f;
+              const float b = in ? elu_bf(v[P][2 * e + 1] + bb0[P][2 * e + 1]) : 0.f;
               o[e] = (int)se_pack(a, b);
             }
             *(i32x4*)(smem + C::O_E1 + (r * C::E1_W + c) * C::E_PITCH + co * 2) = o;
@@ -215,8 +215,8 @@ __global__ __launch_bounds__(512) void segenc_fwd_kernel(const dvie_segenc_desc 
             i32x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float a = in ? act_fwd(v[P][2 * e] + bb2[P][2 * e], DVIE_ACT_ELU, 0.f) : 0.f;
-              const float b = in ? act_fwd(v[P][2 * e + 1] + bb2[P][2 * e + 1], DVIE_ACT_ELU, 0.f) : 0.f;
+              const float a = in ? elu_bf(v[P][2 * e] + bb2[P][2 * e]) : 0.f;
+              const float b = in ? elu_bf(v[P][2 * e + 1] + bb2[P][2 * e + 1]) : 0.f;
               o[e] = (int)se_pack(a, b);
             }
             *(i32x4*)(smem + C::O_E2 + (r * C::E2_W + c) * C::E_PITCH + co * 2) = o;
