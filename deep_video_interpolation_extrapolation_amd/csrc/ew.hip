@@ -40,6 +40,14 @@ __device__ __forceinline__ Lerp lerp_src(int dst, int in_size, int out_size, int
   return r;
 }
 
+typedef __bf16 ew_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float ew_f32x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32; = f2bf for every
+// non-NaN input, a quiet NaN for NaN)
+__device__ __forceinline__ uint32_t ew_pack(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((ew_f32x2{a, b}), ew_bf16x2));
+}
+
 // VW-channel vectors (16 B for bf16 x8 / fp32 x4; 8 B for bf16 x4)
 template <typename T, int VW>
 struct VecN;
@@ -56,7 +64,7 @@ struct VecN<bf16_t, 8> {
   __device__ __forceinline__ static void store(bf16_t* p, const float* v) {
     i32x4 r;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = (int)((uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16));
+    for (int k = 0; k < 4; ++k) r[k] = (int)ew_pack(v[2 * k], v[2 * k + 1]);
     *(i32x4*)p = r;
   }
 };
@@ -412,6 +420,130 @@ __global__ __launch_bounds__(256) void ew_fuse2_kernel(const dvie_ew_desc p, int
   if (two) finish(x + 1, v1);
 }
 
+// EW_UPT (the upsample adjoint) at an integer ratio R (align_corners False), bf16 x8, with two
+// horizontally adjacent coarse outputs per thread: their fine-column windows (2R + 2 each,
+// R apart) overlap, so a fine row costs 3R + 2 loads per pair instead of 4R + 4.  Same
+// weights (upt_weight) and, per output, the same summation order as upt_ratio.  Launched for
+// R = 2 (8x128x256 128-ch: 0.142 -> 0.110 ms/step, 64-ch 0.129 -> 0.115, profiles/r05h/);
+// at R = 4 it measured no gain (0.187 vs 0.190: 172 VGPRs, half the occupancy).
+template <int R>
+__global__ __launch_bounds__(256) void ew_upt2_kernel(const dvie_ew_desc p, int cq) {
+  constexpr int NC = 2 * R + 2, NC2 = 3 * R + 2;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int wp = (p.w + 1) >> 1;
+  if (e >= wp * cq) return;
+  const int xp = e / cq;
+  const int c = (e - xp * cq) * 8;
+  const int x = 2 * xp;
+  const bool two = x + 1 < p.w;
+  const int row = blockIdx.y;
+  const int n = row / p.h, y = row - (row / p.h) * p.h;
+  const int sh = p.sh0, sw = p.sw0;
+  const bf16_t* s = (const bf16_t*)p.src0;
+  const long long ld = p.src_ld0;
+  const int Y0 = R * y - R / 2 - 1, X0 = R * x - R / 2 - 1;
+  // column j of the pair's window: fine X0 + j; pixel x uses j < NC, pixel x + 1 uses j >= R
+  float wx0[NC2], wx1[NC2];
+  unsigned xo[NC2];  // byte offset of the column's 8 channels within a fine row
+#pragma unroll
+  for (int j = 0; j < NC2; ++j) {
+    const int X = X0 + j;
+    const bool in = X >= 0 && X < sw;
+    wx0[j] = (in && j < NC) ? upt_weight(X, x, p.w, sw, 0) : 0.f;
+    wx1[j] = (in && two && j >= R) ? upt_weight(X, x + 1, p.w, sw, 0) : 0.f;
+    xo[j] = (unsigned)((in ? X : 0) * ld + c) * 2u;
+  }
+  // (32-bit buffer offsets: the launch checks the source spans < 4 GB)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)s, 0, 0x7FFFFFF0, 0x00020000);
+  float v0[8], v1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v0[k] = v1[k] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int Y = Y0 + i;
+    if (Y < 0 || Y >= sh) continue;
+    const float wy = upt_weight(Y, y, p.h, sh, 0);
+    if (wy == 0.f) continue;
+    const unsigned rowo = (unsigned)(((long long)n * sh + Y) * sw * ld) * 2u;
+    i32x4 raw[NC2];
+#pragma unroll
+    for (int j = 0; j < NC2; ++j) raw[j] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, rowo + xo[j], 0, 0));
+#pragma unroll
+    for (int j = 0; j < NC2; ++j) {
+      const float g0 = wy * wx0[j], g1 = wy * wx1[j];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = __uint_as_float(((uint32_t)raw[j][k]) << 16), hi = __uint_as_float(((uint32_t)raw[j][k]) & 0xffff0000u);
+        if (j < NC) {
+          v0[2 * k] += g0 * lo;
+          v0[2 * k + 1] += g0 * hi;
+        }
+        if (j >= R) {
+          v1[2 * k] += g1 * lo;
+          v1[2 * k + 1] += g1 * hi;
+        }
+      }
+    }
+  }
+  auto finish = [&](int xx, float* v) {
+    const long long pix = (long long)row * p.w + xx;
+    bf16_t* yp = (bf16_t*)p.y + pix * p.y_ld + c;
+    float t[8];
+    if (p.res) {
+      VecN<bf16_t, 8>::load((const bf16_t*)p.res + pix * p.res_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (p.beta) {
+      VecN<bf16_t, 8>::load(yp, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (p.act) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd(v[k], p.act, p.alpha);
+    }
+    if (p.dact) {
+      VecN<bf16_t, 8>::load((const bf16_t*)p.z + pix * p.z_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= act_dz(t[k], p.dact, p.alpha);
+    }
+    VecN<bf16_t, 8>::store(yp, v);
+  };
+  finish(x, v0);
+  if (two) finish(x + 1, v1);
+}
+
+// EW_NCHW for bf16 x8 without epilogue operands: one PIXEL per thread, consecutive threads on
+// consecutive x, so every planar read (one channel of 64 pixels per wave) is a contiguous
+// 256-B row piece -- the generic kernel's channel-fastest mapping made them 4-byte gathers
+// H x W floats apart.  The thread then writes its pixel's c channels as 16-B vectors.
+__global__ __launch_bounds__(256) void ew_nchw_kernel(const dvie_ew_desc p) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= p.w) return;
+  const int row = blockIdx.y;
+  const int n = row / p.h, y = row - (row / p.h) * p.h;
+  const long long pix = (long long)row * p.w + x;
+  const long long base = (long long)n * p.sn + (long long)y * p.sh + (long long)x * p.sw;
+  for (int c = 0; c < p.c; c += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ch = c + k;
+      float t = 0.f;
+      if (ch < p.ext_c) {
+        const bool second = p.src1 != nullptr && ch >= p.sh1;
+        const float* e = second ? (const float*)p.src1 : p.ext;
+        const int cc = second ? ch - p.sh1 : ch;
+        t = e[base + (long long)cc * p.sc];
+        if (p.mean) t = (t - p.mean[ch]) / p.std[ch];
+      }
+      v[k] = t;
+    }
+    VecN<bf16_t, 8>::store((bf16_t*)p.y + pix * p.y_ld + c, v);
+  }
+}
+
 }  // namespace dvie
 
 using namespace dvie;
@@ -419,6 +551,12 @@ using namespace dvie;
 // DVIE_EW_FUSE2=0: one output pixel per thread for the fuse op (A/B runs); read per launch
 static bool fuse2_on() {
   const char* e = getenv("DVIE_EW_FUSE2");
+  return !(e && *e == '0');
+}
+
+// DVIE_EW_UPT2=0: one coarse output per thread for the integer-ratio upsample adjoint (A/B)
+static bool upt2_on() {
+  const char* e = getenv("DVIE_EW_UPT2");
   return !(e && *e == '0');
 }
 
@@ -449,12 +587,20 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
       // (pairs need every source at most the output's size: a source step <= 1 per pixel)
       const bool up = d->sw0 <= d->w && d->sh0 <= d->h && (d->nsrc < 2 || (d->sw1 <= d->w && d->sh1 <= d->h)) &&
                       (d->nsrc < 3 || (d->sw2 <= d->w && d->sh2 <= d->h));
-      if (d->op == DVIE_EW_FUSE && up && fuse2_on()) {
+      if (d->op == DVIE_EW_NCHW && !d->res && !d->beta && !d->act && !d->dact) {
+        const dim3 gn((unsigned)((d->w + 255) / 256), (unsigned)(d->n * d->h));
+        DVIE_LAUNCH(ew_nchw_kernel, gn, dim3(256), 0, s, *d);
+      } else if (d->op == DVIE_EW_FUSE && up && fuse2_on()) {
         const dim3 g2((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * d->h));
         DVIE_LAUNCH((ew_fuse2_kernel<bf16_t, 8>), g2, dim3(256), 0, s, *d, cq);
       } else if (d->op == DVIE_EW_FUSE)
         DVIE_LAUNCH((ew_kernel<bf16_t, 8, DVIE_EW_FUSE>), grid, dim3(256), 0, s, *d, cq);
-      else if (d->op == DVIE_EW_UPT)
+      else if (d->op == DVIE_EW_UPT && !d->align && upt2_on() &&
+               (unsigned long long)d->n * d->sh0 * d->sw0 * d->src_ld0 * 2ull < 0x7FFFFFF0ull &&
+               (d->sh0 == 2 * d->h && d->sw0 == 2 * d->w)) {
+        const dim3 g2((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * d->h));
+        DVIE_LAUNCH((ew_upt2_kernel<2>), g2, dim3(256), 0, s, *d, cq);
+      } else if (d->op == DVIE_EW_UPT)
         DVIE_LAUNCH((ew_kernel<bf16_t, 8, DVIE_EW_UPT>), grid, dim3(256), 0, s, *d, cq);
       else
         DVIE_LAUNCH((ew_kernel<bf16_t, 8, -2>), grid, dim3(256), 0, s, *d, cq);

@@ -89,6 +89,7 @@ def test_every_op_of_the_bf16_step_matches_its_reference(dev, monkeypatch, batch
     assert {1, 2, 3, 5, 6, 7, 13, 15} <= kinds, kinds
     if (batch, H, W) == (8, 256, 512):
         names = " ".join(per_kernel)
-        for k in ("conv_h8_kernel", "conv_strip_kernel", "conv1x1_kernel", "wgrad_halo_kernel", "wgrad_wide_kernel",
-                  "head3_bwd_kernel", "segenc_bwd_kernel", "pack_kernel", "wreduce_kernel", "ew_fuse2_kernel"):
+        for k in ("conv_h8_kernel", "conv_strip_kernel", "conv1x1_kernel", "conv1x1_ring_kernel", "conv_s2_kernel",
+                  "wgrad_halo_kernel", "wgrad_wide_kernel", "head3_bwd_kernel", "segenc_bwd_kernel", "pack_kernel",
+                  "wreduce_kernel", "ew_fuse2_kernel", "ew_upt2_kernel", "ew_nchw_kernel"):
             assert k in names, (k, sorted(per_kernel))
