@@ -157,20 +157,32 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
     return q;
   };
 
-  // G tile of tile T into G buffer gb
+  // G tile of tile T into G buffer gb.  Per-lane parts (row in the tile, channel chunk) once;
+  // per tile one wave-uniform base and two range limits.
+  constexpr int GQ = (TMO * C::GPI + NW - 1) / NW;
+  unsigned gofs[GQ];
+  int grd[GQ], grm[GQ];
+  bool gok[GQ];
+#pragma unroll
+  for (int q = 0; q < GQ; ++q) {
+    const int pc = wave + NW * q;
+    const int sub = pc / C::GPI, pr = pc - sub * C::GPI;
+    const int row = pr * 8 + lrow;
+    const int ch = 64 * sub + lcs * 8;
+    grd[q] = row / 64;
+    grm[q] = row & 63;
+    gok[q] = pc < TMO * C::GPI && c0 + ch < p.cout;
+    gofs[q] = (unsigned)(grd[q] * p.ow + grm[q]) * grow + (unsigned)ch * 2u;
+  }
   auto issue_g = [&](const TilePos& T, int gb) {
     char* G = smem + gb * C::GSZ;
+    const unsigned base = (unsigned)((T.n * p.oh + T.y0) * p.ow + T.x0) * grow;
+    const int ylim = p.oh - T.y0, xlim = p.ow - T.x0;
 #pragma unroll
-    for (int q = 0; q < (TMO * C::GPI + NW - 1) / NW; ++q) {
+    for (int q = 0; q < GQ; ++q) {
       const int pc = wave + NW * q;
       if (pc < TMO * C::GPI) {
-        const int sub = pc / C::GPI, pr = pc - sub * C::GPI;
-        const int row = pr * 8 + lrow;
-        const int oy = T.y0 + row / 64, ox = T.x0 + (row & 63);
-        const int ch = 64 * sub + lcs * 8;
-        const unsigned o = (oy < p.oh && ox < p.ow && c0 + ch < p.cout)
-                               ? (unsigned)((T.n * p.oh + oy) * p.ow + ox) * grow + (unsigned)ch * 2u
-                               : OOB;
+        const unsigned o = (gok[q] && grd[q] < ylim && grm[q] < xlim) ? base + gofs[q] : OOB;
         lds_dma16(rg, G + pc * 1024, o);
       }
     }
@@ -189,6 +201,46 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
       const int ch = 64 * sub + lcs * 8;
       const bool ok = hx < 64 + TW - 1 && (unsigned)iy < (unsigned)p.ih && (unsigned)ix < (unsigned)p.iw && k0 + ch < p.c;
       const unsigned o = ok ? (unsigned)((T.n * p.ih + iy) * p.iw + ix) * xrow + (unsigned)ch * 2u : OOB;
+      char* dst = smem + 2 * C::GSZ + sub * C::XSUB + (slot * C::XW + piece * 8) * 128;
+      lds_dma16(rx, dst, o);
+    }
+  };
+
+  // The steady-state refill (a tile's PR new halo rows, same column): per-lane column and
+  // channel parts once, per tile one wave-uniform base; the piece -> (row, column block) split
+  // is uniform per piece index (no per-issue divisions).
+  constexpr int XNP = PR * C::XPR;                          // pieces per sub-image
+  constexpr int XQ = (TMI * XNP + NW - 1) / NW;             // pieces per wave
+  unsigned xofs[XQ];
+  int xhx[XQ];
+  bool xok[XQ];
+#pragma unroll
+  for (int q = 0; q < XQ; ++q) {
+    const int pc = wave + NW * q;
+    const int sub = pc / XNP, rem = pc - sub * XNP;
+    const int hr = rem / C::XPR, piece = rem - hr * C::XPR;
+    const int hx = piece * 8 + lrow;
+    const int ch = 64 * sub + lcs * 8;
+    xhx[q] = hx;
+    xok[q] = pc < TMI * XNP && hx < 64 + TW - 1 && k0 + ch < p.c;
+    xofs[q] = (unsigned)(hr * p.iw + hx) * xrow + (unsigned)ch * 2u;
+  }
+  auto issue_x_new = [&](const TilePos& T) {
+    const int h0 = C::HR - PR;
+    const int yb = T.y0 + p.dy0 + h0, xb = T.x0 + p.dx0;
+    const long long base = ((long long)(T.n * p.ih + yb) * p.iw + xb) * (long long)xrow;
+    int ys = (T.y0 + h0) % C::R;
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int pc = wave + NW * q;
+      if (pc >= TMI * XNP) continue;  // (wave-uniform)
+      const int sub = pc / XNP, rem = pc - sub * XNP;
+      const int hr = rem / C::XPR, piece = rem - hr * C::XPR;  // (constants per unrolled q and wave)
+      int slot = ys + hr;
+      slot -= slot >= C::R ? C::R : 0;
+      const bool rowok = (unsigned)(yb + hr) < (unsigned)p.ih;
+      const bool ok = xok[q] && rowok && (unsigned)(xb + xhx[q]) < (unsigned)p.iw;
+      const unsigned o = ok ? (unsigned)(base + (long long)xofs[q]) : OOB;
       char* dst = smem + 2 * C::GSZ + sub * C::XSUB + (slot * C::XW + piece * 8) * 128;
       lds_dma16(rx, dst, o);
     }
@@ -248,7 +300,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
     const bool same_col = has_next && TN.col == T.col;
     if (same_col && !(dbg & 8)) {  // next tile: its G tile and its PR new halo rows
       issue_g(TN, gb ^ 1);
-      issue_x(TN, C::HR - PR, std::integral_constant<int, PR>());
+      issue_x_new(TN);
     }
     const char* G = smem + gb * C::GSZ;
     const char* X = smem + 2 * C::GSZ;
