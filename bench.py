@@ -8,8 +8,8 @@ InterTrainer step body (HRNet fwd, RGBLoss (L1+GDL+SSIM+VGG19) + 30*CE, backward
 gradient all-reduce, Adamax).  Metric: synthesized frames/s (one per clip), whole job.
 
 After the timed region, 2 extra profiling steps time every plan op with HIP events on the
-launch stream; the dominant kernel family (conv_igemm: forward + data-gradient implicit
-GEMM) is reported against the bf16 MFMA peak as `roofline`.  Rank 0 at N=1 also times the
+launch stream; the dominant kernel family (the conv forward + data-gradient kernels) is
+reported against the bf16 MFMA peak as `roofline`.  Rank 0 at N=1 also times the
 CPU oracle (the reference algorithm restated in PyTorch-CPU fp32) on a bounded sample as
 `cpu_baseline`.
 """
@@ -33,7 +33,7 @@ KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwis
 # HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
 # this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
 # per workload; None: no PMC pass on this workload -> "traffic": null
-PMC_DIRS = {"c2": "r04fc/pmc", "c5": None}
+PMC_DIRS = {"c2": "r05full/pmc", "c5": None}
 
 
 
@@ -395,7 +395,7 @@ def main():
                                                      f"profiles/{pmc_dir})" if traffic is not None else None,
                 "algorithmic_bytes_per_launch": round(by / max(1, n)),
                 "kernel": "conv fwd+dgrad family (conv_h8 / conv_halo / conv_strip / conv_narrow / conv_nk / conv1x1 / "
-                          "conv_igemm / head3_bwd / segenc_fwd kernels)",
+                          "conv1x1_ring / conv_s2 / conv_igemm / head3_bwd / segenc_fwd kernels)",
                 "launches_per_step": n // max(1, a.profile_steps),
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
                 "algorithmic_tflop_per_step": round(fl / a.profile_steps / 1e12, 4),

@@ -11,7 +11,7 @@ import json
 import re
 import sys
 
-FAM = [("conv", r"head3_bwd_kernel|segenc_fwd_kernel|conv_narrow_kernel|conv_h8_kernel|conv_halo_kernel|conv_ws_kernel|conv_strip_kernel|conv_nk_kernel|conv1x1_kernel|conv1x1_persist_kernel|conv_igemm_kernel"),
+FAM = [("conv", r"head3_bwd_kernel|segenc_fwd_kernel|conv_narrow_kernel|conv_h8_kernel|conv_halo_kernel|conv_ws_kernel|conv_strip_kernel|conv_nk_kernel|conv1x1_kernel|conv1x1_persist_kernel|conv1x1_ring_kernel|conv_s2_kernel|conv_igemm_kernel"),
        ("wgrad", r"segenc_bwd_kernel|wgrad_halo_kernel|wgrad_kernel|wgrad_wide_kernel")]
 
 
