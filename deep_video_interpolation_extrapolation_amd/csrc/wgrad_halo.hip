@@ -466,19 +466,13 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
 // flat range, a tile is 64 consecutive pixels.  8 waves = 2 (co) x 4 (ci), a wave owns
 // 128 co x 64 ci (4 x 2 accumulators); G and X are double-buffered (128 KB), one barrier per
 // tile.  One partial slab per split, summed by dvie_wgrad_reduce.
-__global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
-                                                         int n_tiles) {
-  constexpr int NW = 8, NSUB = 4, SUB = 64 * 128, TSZ = NSUB * SUB;
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TSZ];
+template <bool DOB>
+__device__ __forceinline__ void wgrad_wide_body(const dvie_wgrad_desc& p, char* smem, int c0, int k0, int split, int t_begin,
+                                                int t_end) {
+  constexpr int NW = 8, NSUB = 4, SUB = 64 * 128, TSZ = NSUB * SUB, PQ = NSUB * 8 / NW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned OOB = 0xFFFFFFF0u;
-  const int npair = n_co * n_ci;
-  const int lid = xcd_chunk(blockIdx.x, gridDim.x);
-  const int pair = lid % npair, split = lid / npair;
-  const int c0 = (pair % n_co) * 256, k0 = (pair / n_co) * 256;
-  const int t_begin = (int)((long long)split * n_tiles / splits);
-  const int t_end = (int)((long long)(split + 1) * n_tiles / splits);
   const long long npix = (long long)p.n * p.oh * p.ow;
   const unsigned long long gbytes = ((unsigned long long)npix - 1) * (unsigned long long)p.g_ld * 2ull + (unsigned long long)p.cout * 2ull;
   const unsigned long long xbytes = ((unsigned long long)npix - 1) * (unsigned long long)p.x_ld * 2ull + (unsigned long long)p.c * 2ull;
@@ -487,19 +481,33 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((const char*)p.x + (size_t)k0 * 2), 0, (int)(xbytes - (unsigned long long)k0 * 2), 0x00020000);
   const unsigned grow = (unsigned)p.g_ld * 2u, xrow = (unsigned)p.x_ld * 2u;
-  // DMA lane geometry as in wgrad_halo_kernel: piece = 8 pixels x 128 B
+  // DMA lane geometry as in wgrad_halo_kernel (piece = 8 pixels x 128 B); the per-lane parts
+  // of the offsets once, per tile one wave-uniform base and a pixel limit
   const int lrow = lane >> 3, lch = lane & 7;
   const int lcs = lch ^ (((lrow >> 1) & 1) << 2);
-  auto issue = [&](int tile, int buf) {
+  int ppx[PQ];
+  unsigned goff[PQ], xoff[PQ];
+  bool gok[PQ], xok[PQ];
 #pragma unroll
-    for (int q = 0; q < NSUB * 8 / NW; ++q) {
+  for (int q = 0; q < PQ; ++q) {
+    const int pc = wave + NW * q, sub = pc >> 3, pr = pc & 7;
+    const int ch = 64 * sub + lcs * 8;
+    ppx[q] = pr * 8 + lrow;
+    goff[q] = (unsigned)ppx[q] * grow + (unsigned)ch * 2u;
+    xoff[q] = (unsigned)ppx[q] * xrow + (unsigned)ch * 2u;
+    gok[q] = c0 + ch < p.cout;
+    xok[q] = k0 + ch < p.c;
+  }
+  auto issue = [&](int tile, int buf) {
+    const int P0 = tile * 64;
+    const int lim = (int)min((long long)64, npix - (long long)P0);
+    const unsigned bg = (unsigned)P0 * grow, bx = (unsigned)P0 * xrow;
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
       const int pc = wave + NW * q, sub = pc >> 3, pr = pc & 7;
-      const long long P = (long long)tile * 64 + pr * 8 + lrow;
-      const int ch = 64 * sub + lcs * 8;
-      const unsigned og = P < npix && c0 + ch < p.cout ? (unsigned)P * grow + (unsigned)ch * 2u : OOB;
-      const unsigned ox = P < npix && k0 + ch < p.c ? (unsigned)P * xrow + (unsigned)ch * 2u : OOB;
-      lds_dma16(rg, smem + buf * TSZ + sub * SUB + pr * 1024, og);
-      lds_dma16(rx, smem + (2 + buf) * TSZ + sub * SUB + pr * 1024, ox);
+      const bool in = ppx[q] < lim;
+      lds_dma16(rg, smem + buf * TSZ + sub * SUB + pr * 1024, (in && gok[q]) ? bg + goff[q] : OOB);
+      lds_dma16(rx, smem + (2 + buf) * TSZ + sub * SUB + pr * 1024, (in && xok[q]) ? bx + xoff[q] : OOB);
     }
   };
   const int grp = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
@@ -509,7 +517,6 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
     return tq * 128 + ch * 16 + (col & 7) * 2 + 8 * 128 * (grp >> 1);
   };
   const int wco = wave >> 2, wci = wave & 3;
-  const bool dob = p.bws != nullptr && k0 == 0 && wci == 0;  // bias column sums, as in wgrad_halo_kernel
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};
   int g_off[4], x_off[2];
 #pragma unroll
@@ -551,13 +558,15 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[j], b[i], acc[j][i], 0, 0, 0);
+      if constexpr (DOB) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bsum[j] = sum8_bf16(a[j], bsum[j]);  // (unconditional, as above)
+        for (int j = 0; j < 4; ++j) bsum[j] = sum8_bf16(a[j], bsum[j]);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
-  if (dob) {
+  if constexpr (DOB) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float t = bsum[j] + __shfl_xor(bsum[j], 32, 64);
@@ -581,6 +590,25 @@ __global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p
         if (co < p.cout) slab[(long long)co * p.c + ci] = acc[j][i][e];
       }
     }
+}
+
+__global__ __launch_bounds__(512) void wgrad_wide_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
+                                                         int n_tiles) {
+  __shared__ __attribute__((aligned(1024))) char smem[4 * 4 * 64 * 128];
+  const int npair = n_co * n_ci;
+  const int lid = xcd_chunk(blockIdx.x, gridDim.x);
+  const int pair = lid % npair, split = lid / npair;
+  const int c0 = (pair % n_co) * 256, k0 = (pair / n_co) * 256;
+  const int t_begin = (int)((long long)split * n_tiles / splits);
+  const int t_end = (int)((long long)(split + 1) * n_tiles / splits);
+  // bias column sums (the ci-block-0 workgroups' wci = 0 waves, from the G fragments they hold
+  // for the MFMAs): compiled as its own body, so the other waves and workgroups carry none of
+  // the summing (a wave-uniform choice, made once)
+  const int wci = (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) & 3;
+  if (p.bws != nullptr && k0 == 0 && wci == 0)
+    wgrad_wide_body<true>(p, smem, c0, k0, split, t_begin, t_end);
+  else
+    wgrad_wide_body<false>(p, smem, c0, k0, split, t_begin, t_end);
 }
 
 // diagnostic override, read once (plan-time slab counts and launches must agree):
