@@ -65,6 +65,34 @@ __device__ __forceinline__ void unpack8(const i32x4 t, float* v) {
   }
 }
 
+// 8 x 8 transpose of 16-B chunks inside each 8-lane group: (lane b, chunk k) <-> (lane k,
+// chunk b); at distance d the lane with bit d set trades its chunk k for the partner's chunk
+// k + d.  An involution: applied to chunks loaded in the transposed (row-coalesced) layout it
+// yields the MFMA layout, applied to MFMA-layout results it yields whole-row stores.
+// (element-wise selects on the lane bit, so every array index is a constant and the chunks
+// stay in registers)
+__device__ __forceinline__ void transpose8x8(i32x4 (&ob)[8], int lane) {
+  const int b = lane & 7;
+#pragma unroll
+  for (int d = 4; d >= 1; d >>= 1) {
+    const bool up = (b & d) != 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k & d) continue;
+      i32x4 t, r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = up ? ob[k][e] : ob[k + d][e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = __shfl_xor(t[e], d);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ob[k][e] = up ? r[e] : ob[k][e];
+        ob[k + d][e] = up ? ob[k + d][e] : r[e];
+      }
+    }
+  }
+}
+
 // KC = input channels per K-step (64: 128-byte LDS rows, 32: 64-byte rows, half the stage
 // bytes, so the same LDS holds twice the stages in flight).  A DMA piece is always 1 KB:
 // RPP rows of RB bytes.
@@ -194,7 +222,32 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
   // c0 + wc*32*TMC + 32*j + 16*P + 8*h .. +7); identity output placement only (checked at launch)
   static_assert(PRE == 0 || (NS == 1 && !OUTF32), "operand prefetch: single K-step, bf16 output");
   i32x4 pr_r[(PRE & 1) ? MI : 1][TMC][2], pr_b[(PRE & 2) ? MI : 1][TMC][2], pr_z[(PRE & 4) ? MI : 1][TMC][2];
-  if constexpr (PRE != 0) {
+  // CE tiles with two or more operands (layer1's 256-channel data gradients: residual +
+  // activation input) load them row-coalesced: 0.47 -> 0.43 ms each; with a single operand
+  // the transposes' extra registers cost an occupancy step (121 -> 148 VGPRs) and the
+  // forward with a residual measured 0.247 -> 0.290 ms (profiles/r05l/)
+  constexpr bool CEL = CE && (PRE & (PRE - 1)) != 0;
+  if constexpr (CEL) {
+    // CE tiles: the operands are loaded in the transposed layout of the CE stores -- lane
+    // (h, 8 a + b), chunk k = pixel 8 a + k, channels 16 b + 8 h of the wave's 128 -- so each
+    // load instruction reads 4 pixels x 256 contiguous bytes; transpose8x8 (epilogue) turns
+    // them into the MFMA layout.  (CE: MI = 1, 8 chunks, full channel tiles.)
+    const int wp0 = wave % NWP, wc0 = wave / NWP;
+    const int a8 = r32 >> 3, bl = lane & 7;
+    const int co = c0 + wc0 * 32 * TMC + 16 * bl + 8 * hh;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int pix = p0 + wp0 * 32 + 8 * a8 + k;
+      const bool ok = pix < npix;
+      const long long q = ok ? pix : 0;
+      if constexpr ((PRE & 1) != 0)
+        pr_r[0][k >> 1][k & 1] = ok ? *(const i32x4*)((const bf16_t*)p.res + q * p.res_ld + co) : i32x4{0, 0, 0, 0};
+      if constexpr ((PRE & 2) != 0)
+        pr_b[0][k >> 1][k & 1] = ok ? *(const i32x4*)((const bf16_t*)p.y + q * p.y_ld + co) : i32x4{0, 0, 0, 0};
+      if constexpr ((PRE & 4) != 0)
+        pr_z[0][k >> 1][k & 1] = ok ? *(const i32x4*)((const bf16_t*)p.z + q * p.z_ld + co) : i32x4{0, 0, 0, 0};
+    }
+  } else if constexpr (PRE != 0) {
     const int wp0 = wave % NWP, wc0 = wave / NWP;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -261,6 +314,19 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
   // ---- epilogue: lane owns pixel wp*32*MI + 32*i + r32; after permlane32 pairing, lane half h
   // holds channels 16P + 8h .. +7 of pair P of each 32-channel accumulator
   static_assert(!CE || (MI == 1 && 2 * TMC == 8 && !OUTF32), "coalesced epilogue: 8 chunks per lane");
+  if constexpr (CEL) {  // the row-coalesced operand loads into the MFMA layout
+    auto tr = [&](i32x4 (&a)[TMC][2]) {
+      i32x4 t8[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t8[k] = a[k >> 1][k & 1];
+      transpose8x8(t8, lane);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k >> 1][k & 1] = t8[k];
+    };
+    if constexpr ((PRE & 1) != 0) tr(pr_r[0]);
+    if constexpr ((PRE & 2) != 0) tr(pr_b[0]);
+    if constexpr ((PRE & 4) != 0) tr(pr_z[0]);
+  }
   i32x4 ob[CE ? 8 : 1];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
@@ -366,25 +432,8 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
     }
   }
   if constexpr (CE) {
-    // 8 x 8 transpose of 16-B chunks inside each 8-lane group (lane b, chunk k) -> (k, b):
-    // at distance d the lane with bit d set trades its chunk k for the partner's chunk k + d
+    transpose8x8(ob, lane);
     const int b = lane & 7;
-#pragma unroll
-    for (int d = 4; d >= 1; d >>= 1) {
-      const bool up = (b & d) != 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (k & d) continue;
-        const i32x4 t = up ? ob[k] : ob[k + d];
-        i32x4 r;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] = __shfl_xor(t[e], d);
-        if (up)
-          ob[k] = r;
-        else
-          ob[k + d] = r;
-      }
-    }
     // lane (h, 8a + b) now holds pixel 8a + k, channels 32 (b / 2) + 16 (b % 2) + 8 h of chunk k
     const int a8 = r32 >> 3;
 #pragma unroll
