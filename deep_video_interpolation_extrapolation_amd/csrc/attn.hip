@@ -784,15 +784,132 @@ __global__ __launch_bounds__(256) void attn_corr_mfma_kernel(const dvie_attn_des
   }
 }
 
+// ---- CORR in one-barrier stages for c <= 128 (the refinement nets' 128-channel features) ----
+// attn_corr_mfma_kernel stages one (64-channel chunk, window row) per stage behind two
+// barriers and adds every chunk's band into its LDS rows.  Here K = channels runs over ALL
+// channels inside a stage (two 64-channel planes of 128-B rows), so a stage is one (map,
+// window row), its band entries are complete after its MFMAs and are written (not added) to
+// the LDS output rows; the source rows are double-buffered in LDS, one barrier per stage.
+// C5 (profiles/r05o/): corr 0.212 -> 0.159 ms, the prob gradient 0.143 -> 0.102.  Measured
+// dead ends: the same one-barrier form of GATHER / GATHER_T (all channels and one map per
+// stage, 63.5 KB: gathers 0.358 -> 0.475 ms), loads two stages ahead (two register sets) in
+// both kernels, and XCD-contiguous tile ranges (gathers 0.475 -> 0.443 but CORR 0.159 ->
+// 0.188 and the gradients' gathers 1.139 -> 1.253).
+constexpr int A2_CP = 2;                                          // channel planes: c <= 128
+constexpr int A2_SB = A2_CP * CM_SP * 128;                        // staged source row, all planes
+
+constexpr int A2_CA = A2_CP * CM_TP * 128;  // the tile's pixel rows, all planes
+static_assert(A2_CA + 2 * A2_SB + CM_TP * CM_J * 4 <= 81920, "two corr workgroups per CU");
+
+__global__ __launch_bounds__(256, 2) void attn_corr_mfma2_kernel(const dvie_attn_desc p) {
+  __shared__ __attribute__((aligned(16))) char sA[A2_CA];
+  __shared__ __attribute__((aligned(16))) char sB[2 * A2_SB];
+  __shared__ float sO[CM_TP * CM_J];
+  const Tile t = tile_of(p.w, p.h);
+  const int K = p.wh * p.ww, rh = p.wh / 2, rw = p.ww / 2, J = p.nhalf * K;
+  const bf16_t* maps[2] = {(const bf16_t*)p.b0, (const bf16_t*)p.b1};
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int pb = wave & 1, sb = wave >> 1;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const long long pix0 = ((long long)t.n * p.h + t.y) * p.w + t.x0;
+  const int npx = min(CM_TP, p.w - t.x0);
+  const int ncp = (p.c + 63) / 64;
+  const int srow = min(32 * pb + 32 * sb + r32, CM_SP - 1), prow = 32 * pb + r32;
+  // live maps (a missing map's entries are written as zeros): lm0, and lm1 when both are present
+  const bool live1 = p.nhalf > 1 && p.b1;
+  const int nlive = (p.b0 ? 1 : 0) + (live1 ? 1 : 0);
+  const int lm0 = p.b0 ? 0 : 1;
+  const int nstage = nlive * p.wh;
+  i32x4 pv[5];
+  auto fetch = [&](int st) {
+    const int m = st / p.wh ? 1 : lm0, r = st % p.wh, yy = t.y + r - rh;
+    const bool rowin = (unsigned)yy < (unsigned)p.h;
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int i = tid + 256 * u, s = i >> 4, ck = i & 15;
+      const int x = t.x0 - rw + s, ch = 8 * ck;
+      pv[u] = i32x4{0, 0, 0, 0};
+      if (s < CM_TP + 2 * rw && rowin && (unsigned)x < (unsigned)p.w && ch < p.c)
+        pv[u] = *(const i32x4*)(maps[m] + (((long long)t.n * p.h + yy) * p.w + x) * p.b_ld + ch);
+    }
+  };
+  auto store = [&](int buf) {
+    char* B = sB + buf * A2_SB;
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int i = tid + 256 * u, s = i >> 4, ck = i & 15, pl = ck >> 3, c8 = ck & 7;
+      *(i32x4*)(B + pl * CM_SP * 128 + s * 128 + ((c8 ^ ((s >> 1) & 7)) << 4)) = pv[u];
+    }
+  };
+  // the tile's pixel rows (all channels), once
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + 256 * u, q = i >> 4, ck = i & 15, pl = ck >> 3, c8 = ck & 7, ch = 8 * ck;
+    i32x4 v = {0, 0, 0, 0};
+    if (q < npx && ch < p.c) v = *(const i32x4*)((const bf16_t*)p.a + (pix0 + q) * p.a_ld + ch);
+    *(i32x4*)(sA + pl * CM_TP * 128 + q * 128 + ((c8 ^ ((q >> 1) & 7)) << 4)) = v;
+  }
+  if (nstage > 0) {
+    fetch(0);
+    store(0);
+  }
+  __syncthreads();
+  // stage st: compute from buffer st & 1, the next stage's rows loaded into registers under
+  // the MFMAs and written to the other buffer (its last readers passed the previous barrier)
+  for (int st = 0; st < nstage; ++st) {
+    const int m = st / p.wh ? 1 : lm0, r = st % p.wh;
+    if (st + 1 < nstage) fetch(st + 1);
+    const char* B = sB + (st & 1) * A2_SB;
+    f32x16 acc = {};
+#pragma unroll
+    for (int pl = 0; pl < A2_CP; ++pl) {
+      if (pl >= ncp) continue;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int ck = 2 * ks + hh;
+        const i32x4 av = *(const i32x4*)(B + pl * CM_SP * 128 + srow * 128 + ((ck ^ ((srow >> 1) & 7)) << 4));
+        const i32x4 bv = *(const i32x4*)(sA + pl * CM_TP * 128 + prow * 128 + ((ck ^ ((prow >> 1) & 7)) << 4));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, bv), acc,
+                                                      0, 0, 0);
+      }
+    }
+    // lane: pixel prow (column), sources 32 pb + 32 sb + 8 (e / 4) + 4 hh + e % 4 (rows); each
+    // band entry (s - prow in [0, ww)) belongs to exactly one lane of one wave
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int s = 32 * pb + 32 * sb + 8 * (e >> 2) + 4 * hh + (e & 3);
+      const int kc = s - prow;
+      if (kc >= 0 && kc < p.ww) sO[prow * CM_J + m * K + r * p.ww + kc] = acc[e];
+    }
+    if (st + 1 < nstage) store((st + 1) & 1);
+    __syncthreads();
+  }
+  // outputs: (pixel, entry) pairs advanced by 256 without divisions
+  int q = tid / J, j = tid - (tid / J) * J;
+  const int dq = 256 / J, dj = 256 - dq * J;
+  for (int e = tid; e < npx * J; e += 256) {
+    const bool live = j < K ? p.b0 != nullptr : live1;
+    epi1<bf16_t>(p, pix0 + q, j, live ? sO[q * CM_J + j] : 0.f);
+    q += dq;
+    j += dj;
+    if (j >= J) {
+      j -= J;
+      ++q;
+    }
+  }
+}
+
 }  // namespace dvie
 
 using namespace dvie;
 
-// DVIE_ATTN_MFMA=0: the VALU window kernels for GATHER / GATHER_T / CORR (A/B runs); read per launch
-static bool gm_on() {
+// DVIE_ATTN_MFMA (A/B runs, read per launch): 0 = the VALU window kernels for GATHER /
+// GATHER_T / CORR, 2 = the chunked two-barrier CORR kernel at every channel count
+static int gm_mode() {
   const char* e = getenv("DVIE_ATTN_MFMA");
-  return !(e && *e == '0');
+  return e && *e == '0' ? 0 : e && *e == '2' ? 2 : 1;
 }
+static bool gm_on() { return gm_mode() != 0; }
 
 extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->a && d->y, "attn: null pointer");
@@ -858,7 +975,10 @@ extern "C" int dvie_attn(const dvie_attn_desc* d, void* stream) {
       DVIE_CHECK_ARG(d->c > 0 && d->c % 4 == 0, "attn: corr c=%d", d->c);
       DVIE_CHECK_ARG(d->y_ld >= d->nhalf * K, "attn: corr y_ld");
       if (tiled && bf && d->c % 32 == 0 && d->a_ld % 8 == 0 && d->b_ld % 8 == 0 && gm_on()) {
-        DVIE_LAUNCH(attn_corr_mfma_kernel, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        if (d->c <= 64 * A2_CP && gm_mode() == 1)
+          DVIE_LAUNCH(attn_corr_mfma2_kernel, dim3((unsigned)tiles), dim3(256), 0, s, *d);
+        else
+          DVIE_LAUNCH(attn_corr_mfma_kernel, dim3((unsigned)tiles), dim3(256), 0, s, *d);
         break;
       }
       if (tiled) {

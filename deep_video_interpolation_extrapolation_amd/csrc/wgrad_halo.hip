@@ -87,7 +87,10 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 // PIPE: the next k-step's fragments (its G fragment and all NT * TMI shifted X fragments) are
 // read from LDS while the current k-step's MFMAs run (two fragment sets in registers), instead
 // of each MFMA waiting on the transposed reads issued just before it.
-template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8, bool PIPE = false>
+// AB: timing-only ablations, compiled into -DDVIE_TIMING_DBG builds only (DVIE_WG_DBG): 8 = no
+// DMA after the first tile (stale operands), 16 = no MFMAs, 32 = no slab stores, 64 = no LDS
+// fragment reads after a tile's first two k-steps, 128 = no end-of-tile wait and barrier
+template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8, bool PIPE = false, int AB = 0>
 __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
                                                              int tiles_x, int tiles_y, int n_tiles, int flags) {
   typedef WgCfg<TH, TW, PR, TMO, TMI> C;
@@ -97,9 +100,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int merge = flags & 1;
-  // timing-only ablations (-DDVIE_TIMING_DBG builds, DVIE_WG_DBG): 8 = no DMA after the first
-  // tile (stale operands), 16 = no MFMAs, 32 = no slab stores
-  const int dbg = DVIE_DBG(flags & 56);
+  constexpr int dbg = AB;  // (timing-only ablation bits, above)
   // flags bit 1: static priority for the second-dispatched half of the waves (the arbitration
   // loser on every MFMA/VALU segment, MI355X_MICROARCH "Two waves per SIMD" item 4)
   if ((flags & 2) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
@@ -309,6 +310,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
       const int ys = T.y0 % C::R;  // ring slot of the tile's first halo row
       bf16x8 pa[2][TMO], pb[2][NB];
       auto load = [&](int st, int k) {
+        if ((dbg & 64) && st >= 2) return;
         const int py = wrow * (PR / 2) + (st >> 2), kx = st & 3;
         const int gr = py * 64 + kx * 16;
 #pragma unroll
@@ -398,8 +400,10 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
 #pragma unroll
         for (int j = 0; j < TMO; ++j) bsum[j] = sum8_bf16(a[j], bsum[j]);
       }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+    if (!(dbg & 128)) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
     if (has_next && !same_col) {  // column change: refill the whole ring (pipeline restart)
       issue_g(TN, gb ^ 1);
       issue_x(TN, 0, std::integral_constant<int, C::HR>());
@@ -687,7 +691,7 @@ static const int wg_merge = getenv("DVIE_WG_MERGE") && *getenv("DVIE_WG_MERGE") 
 static int wg_dbg() {
 #ifdef DVIE_TIMING_DBG
   const char* e = getenv("DVIE_WG_DBG");
-  return e && *e ? (atoi(e) & 56) : 0;
+  return e && *e ? atoi(e) : 0;
 #else
   return 0;
 #endif
@@ -725,12 +729,27 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   }
 #define DVIE_WG(TH, PR, TMO, TMI)                                                                                   \
   DVIE_LAUNCH((wgrad_halo_kernel<TH, TH, PR, TMO, TMI>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
-                     tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio | wg_dbg())
+                     tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio)
+#ifdef DVIE_TIMING_DBG
+  if (p.th == 3 && p.cout > 32 && wg_pipe && wg_dbg()) {
+    switch (wg_dbg()) {
+#define DVIE_WG_AB(V)                                                                                             \
+  case V:                                                                                                         \
+    DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true, V>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
+                tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);                                                 \
+    return true;
+      DVIE_WG_AB(8) DVIE_WG_AB(16) DVIE_WG_AB(32) DVIE_WG_AB(64) DVIE_WG_AB(128) DVIE_WG_AB(136) DVIE_WG_AB(80)
+      DVIE_WG_AB(192) DVIE_WG_AB(144)
+#undef DVIE_WG_AB
+      default: break;
+    }
+  }
+#endif
   if (p.th == 3 && p.cout > 32 && wg_pipe)
     DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
-                       tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio | wg_dbg());
+                       tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   else if (p.th == 3 && p.cout <= 32 && !wg_narrow_env_off)
-    DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 4>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
+    DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 4, true>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   else if (p.th == 3)
     DVIE_WG(3, 4, 1, 1);

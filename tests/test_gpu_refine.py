@@ -124,20 +124,24 @@ def test_attention_ops_bf16_close_to_fp32(dev, prop):
         assert torch.isfinite(g16[k]).all() and rel_l2(g16[k], g32[k]) < 3e-2, (k, rel_l2(g16[k], g32[k]))
 
 
-@pytest.mark.parametrize("shape", [(1, 128, 9, 150), (2, 64, 6, 70)])
+@pytest.mark.parametrize("shape", [(1, 128, 9, 150), (2, 64, 6, 70), (1, 96, 7, 130), (1, 160, 5, 70)])
 def test_attention_gather_mfma_matches_valu(dev, shape, monkeypatch):
-    """bf16 GATHER on the matrix cores (band GEMMs over the staged source rows, the default
-    for c % 32 == 0) against the VALU window kernel (DVIE_ATTN_MFMA=0): the same bf16
-    products summed in another fp32 order, so outputs and input gradients within 1e-2
-    relative L2 (bf16 output rounding); two maps and single-map (half0 0 / 1) gathers, ragged
-    last row tiles, windows clipped at the borders."""
+    """bf16 GATHER / GATHER_T / CORR on the matrix cores (band GEMMs over the staged source
+    rows, the default for c % 32 == 0) against the VALU window kernels (DVIE_ATTN_MFMA=0):
+    the same bf16 products summed in another fp32 order, so outputs and input gradients within
+    1e-2 relative L2 (bf16 output rounding).  Both matrix-core CORR forms: the one-barrier
+    all-channel stages (default, c <= 128; c = 160 takes the chunked form) and the chunked
+    two-barrier form (DVIE_ATTN_MFMA=2).  Two maps and single-map (half0 0 / 1) gathers, a
+    half-used second channel plane (96), ragged last row tiles, windows clipped at the
+    borders."""
     res = {}
-    for env in ("1", "0"):
+    for env in ("1", "2", "0"):
         monkeypatch.setenv("DVIE_ATTN_MFMA", env)
         res[env] = _run_attn(dev, torch.bfloat16, *shape, True)
-    for a, b in ((res["1"][2], res["0"][2]), (res["1"][3], res["0"][3])):
-        for k in b:
-            assert torch.isfinite(a[k]).all() and rel_l2(a[k], b[k]) < 1e-2, (k, rel_l2(a[k], b[k]))
+    for env in ("1", "2"):
+        for a, b in ((res[env][2], res["0"][2]), (res[env][3], res["0"][3])):
+            for k in b:
+                assert torch.isfinite(a[k]).all() and rel_l2(a[k], b[k]) < 1e-2, (env, k, rel_l2(a[k], b[k]))
 
 
 def _grads(P, names):
