@@ -425,41 +425,46 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
 
   // ---- partial slab ws[split][co][t*c + ci] ----
   // The two row halves are summed through LDS first (one slab per split: half the slab
-  // writes and half the reduction's reads).  Per tap, the wrow = 1 waves park their
-  // accumulators lane-fastest (conflict-free), the wrow = 0 partner adds and stores.
+  // writes and half the reduction's reads).  Each row half owns half the taps: a wave parks
+  // the taps its partner owns (lane-fastest, conflict-free), one barrier, and adds the parked
+  // values to its own taps as it stores them -- both halves store, behind a single barrier.
   // C layout: column (ci) = lane & 31, rows (co) = 8*(e>>2) + 4*(lane>>5) + (e&3)
   const long long ws_k = (long long)C::NT * p.c;
   const int r32 = lane & 31, hh = lane >> 5;
   float* slab = p.ws + (long long)(merge ? split : 2 * split + wrow) * p.cout * ws_k;
-  static_assert(4 * TMO * TMI * 16 * 64 * 4 <= C::SMEM, "row-half exchange fits the LDS");
-  float* X = (float*)smem + (wco * 2 + wci) * (TMO * TMI * 16 * 64) + lane;
+  constexpr int TO = (C::NT + 1) / 2;  // taps [0, TO) are row half 0's, [TO, NT) row half 1's
+  constexpr int PSZ = TMO * TMI * 16 * 64;  // floats per parked tap of one wave
+  static_assert((NW / 2) * C::NT * PSZ * 4 <= C::SMEM, "row-half exchange fits the LDS");
+  float* X = (float*)smem + (wco * 2 + wci) * (C::NT * PSZ) + lane;
+  if (merge) {
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t)
+      if ((t < TO) != (wrow == 0)) {
+#pragma unroll
+        for (int j = 0; j < TMO * TMI; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) X[t * PSZ + (j * 16 + e) * 64] = acc[t * TMO * TMI + j][e];
+      }
+    __syncthreads();
+  }
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) {
-    if (merge && wrow == 1) {
+    if (merge && (t < TO) != (wrow == 0)) continue;
 #pragma unroll
-      for (int j = 0; j < TMO * TMI; ++j)
+    for (int jo = 0; jo < TMO; ++jo)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) X[(j * 16 + e) * 64] = acc[t * TMO * TMI + j][e];
-    }
-    if (merge) __syncthreads();
-    if (!merge || wrow == 0) {
+      for (int ji = 0; ji < TMI; ++ji) {
+        const int ci = k0 + wci * 32 * TMI + 32 * ji + r32;
+        if (ci >= p.c) continue;
+        const int j = jo * TMI + ji;
 #pragma unroll
-      for (int jo = 0; jo < TMO; ++jo)
-#pragma unroll
-        for (int ji = 0; ji < TMI; ++ji) {
-          const int ci = k0 + wci * 32 * TMI + 32 * ji + r32;
-          if (ci >= p.c) continue;
-          const int j = jo * TMI + ji;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int co = c0 + wco * 32 * TMO + 32 * jo + 8 * (e >> 2) + 4 * hh + (e & 3);
-            if (co < p.cout && (!(dbg & 32) || acc[t * TMO * TMI + j][e] == 12345.678f))
-              slab[(long long)co * ws_k + (long long)t * p.c + ci] =
-                  acc[t * TMO * TMI + j][e] + (merge ? X[(j * 16 + e) * 64] : 0.f);
-          }
+        for (int e = 0; e < 16; ++e) {
+          const int co = c0 + wco * 32 * TMO + 32 * jo + 8 * (e >> 2) + 4 * hh + (e & 3);
+          if (co < p.cout && (!(dbg & 32) || acc[t * TMO * TMI + j][e] == 12345.678f))
+            slab[(long long)co * ws_k + (long long)t * p.c + ci] =
+                acc[t * TMO * TMI + j][e] + (merge ? X[t * PSZ + (j * 16 + e) * 64] : 0.f);
         }
-    }
-    if (merge) __syncthreads();
+      }
   }
 }
 
