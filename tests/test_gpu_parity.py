@@ -135,6 +135,32 @@ def test_vgg_loss(dev, prec, monkeypatch):
     assert rel_err(g, gr) < (1e-3 if prec == "fp32" else 1e-1)
 
 
+@pytest.mark.parametrize("shape", [(2, 5, 7, 64, 64), (3, 4, 9, 24, 40), (2, 3, 5, 20, 24)])
+def test_feature_l1_nhwc_bf16(dev, shape):
+    """The plan's VGG feature-L1 value (dvie_loss kind L1NHWC, losses.py:157-180) on bf16 NHWC
+    maps (B, H, W, ch of a C-channel buffer) against float64 torch on the same bf16 values:
+    dense rows with ch % 8 == 0 take the 16-byte kernel (also as a channel region of a wider
+    buffer), ch = 20 the per-element one; both within 1e-6 relative."""
+    import ctypes
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    B, H, W, ch, C = shape
+    g = torch.Generator().manual_seed(7)
+    a = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev)
+    b = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16).to(dev)
+    lib = L.load()
+    d = L.LossDesc()
+    d.kind, d.a, d.b, d.dtype = L.LOSS_L1NHWC, a.data_ptr(), b.data_ptr(), L.BF16
+    d.a_sn, d.a_sc, d.a_sh, d.a_sw = H * W * C, 1, W * C, C
+    d.b_sn, d.b_sc, d.b_sh, d.b_sw = H * W * C, 1, W * C, C
+    d.bsz, d.ch, d.h, d.w, d.weight, d.out_scale = B, ch, H, W, 1.0, 1.0
+    part = torch.empty(max(1, lib.dvie_loss_partial_count(ctypes.byref(d))), dtype=torch.float64, device=dev)
+    out = torch.empty(1, dtype=torch.float32, device=dev)
+    d.partial, d.out = part.data_ptr(), out.data_ptr()
+    L.check(lib.dvie_loss(ctypes.byref(d), L.stream_ptr(dev)), "l1nhwc")
+    ref = (a[..., :ch].double() - b[..., :ch].double()).abs().mean().item()
+    assert abs(float(out.item()) - ref) <= 1e-6 * ref, (float(out.item()), ref)
+
+
 def test_vgg_repacks_changed_weights(dev, monkeypatch):
     """The frozen VGG19 plan packs its weights once (Plan.static_weights); an in-place weight
     update (new version counter) must be repacked: the loss after scaling features.0 by 2
