@@ -525,6 +525,25 @@ __global__ __launch_bounds__(256) void ew_nchw_kernel(const dvie_ew_desc p) {
   const int n = row / p.h, y = row - (row / p.h) * p.h;
   const long long pix = (long long)row * p.w + x;
   const long long base = (long long)n * p.sn + (long long)y * p.sh + (long long)x * p.sw;
+  if (p.c <= 32) {  // every planar load issued before the first store (the stores may alias)
+    float v[32];
+#pragma unroll
+    for (int ch = 0; ch < 32; ++ch) {
+      float t = 0.f;
+      if (ch < p.c && ch < p.ext_c) {
+        const bool second = p.src1 != nullptr && ch >= p.sh1;
+        const float* e = second ? (const float*)p.src1 : p.ext;
+        const int cc = second ? ch - p.sh1 : ch;
+        t = e[base + (long long)cc * p.sc];
+        if (p.mean) t = (t - p.mean[ch]) / p.std[ch];
+      }
+      v[ch] = t;
+    }
+#pragma unroll
+    for (int c = 0; c < 32; c += 8)
+      if (c < p.c) VecN<bf16_t, 8>::store((bf16_t*)p.y + pix * p.y_ld + c, v + c);
+    return;
+  }
   for (int c = 0; c < p.c; c += 8) {
     float v[8];
 #pragma unroll

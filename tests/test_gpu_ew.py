@@ -86,12 +86,14 @@ def test_fuse_upsample(dev, case, pairs, monkeypatch):
     assert err < 1e-2, (case, err)
 
 
+@pytest.mark.parametrize("c", [24, 40])
 @pytest.mark.parametrize("norm", [False, True])
-def test_nchw_pack(dev, norm):
+def test_nchw_pack(dev, norm, c):
     """EW_NCHW: fp32 NCHW planes (ext_c of c channels, optional (x - mean) / std as
     preprocess_norm, utils/net_utils.py:11-23) into a bf16 NHWC channel slice; zero channels
-    past ext_c."""
-    n, ec, H, W, c = 2, 6, 37, 301, 24
+    past ext_c.  c <= 32 loads every plane before the first store, c = 40 takes the 8-channel
+    loop."""
+    n, ec, H, W = 2, 6, 37, 301
     g = torch.Generator().manual_seed(11)
     x = torch.randn(n, ec, H, W, generator=g)
     mean = torch.tensor([0.4, 0.5, 0.6, 0.1, 0.2, 0.3] + [0.0] * 2)
