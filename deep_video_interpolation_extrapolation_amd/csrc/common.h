@@ -123,6 +123,18 @@ __device__ __forceinline__ float act_bf(float v, int act, float alpha) {
   }
 }
 
+// the same activations for fp32-output epilogues (fp32 head outputs of a bf16 plan): libm
+// expm1f / tanhf, not the short forms above, which are accurate to bf16 rounding only
+__device__ __forceinline__ float act_f32(float v, int act, float alpha) {
+  switch (act) {
+    case DVIE_ACT_LRELU: return v > 0.f ? v : v * alpha;
+    case DVIE_ACT_ELU: return v > 0.f ? v : expm1f(v);
+    case DVIE_ACT_RELU: return v > 0.f ? v : 0.f;
+    case DVIE_ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
 // derivative expressed through the activation OUTPUT z
 __device__ __forceinline__ float act_dz(float z, int act, float alpha) {
   switch (act) {

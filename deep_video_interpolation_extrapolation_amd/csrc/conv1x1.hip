@@ -386,7 +386,7 @@ __global__ __launch_bounds__(64 * NWP * NWC) void conv1x1_kernel(const dvie_conv
             w[4 + e] += r1[e];
           }
         }
-        act1(w, p.act, p.alpha);
+        for (int k = 0; k < 8; ++k) w[k] = act_f32(w[k], p.act, p.alpha);
         if (p.dact) {
           float z[8];
           unpack8(*(const i32x4*)((const bf16_t*)p.z + yp * p.z_ld + co), z);

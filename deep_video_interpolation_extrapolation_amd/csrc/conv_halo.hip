@@ -50,15 +50,18 @@ __device__ __forceinline__ int xcd_remap3(int b, int nb) {
   return start + i;
 }
 
+// F32OUT: the epilogue stores fp32 (e.g. the fp32 head outputs of a bf16 plan): ELU / tanh
+// through expm1f / tanhf; the short v_exp_f32 forms (common.h) are for bf16 stores only
+template <bool F32OUT = false>
 __device__ __forceinline__ void act_apply(float* v, int n, int act, float alpha) {
   if (act == DVIE_ACT_LRELU) {
     for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : v[k] * alpha;
   } else if (act == DVIE_ACT_RELU) {
     for (int k = 0; k < n; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
   } else if (act == DVIE_ACT_ELU) {
-    for (int k = 0; k < n; ++k) v[k] = elu_bf(v[k]);  // (bf16-output kernels only: common.h)
+    for (int k = 0; k < n; ++k) v[k] = F32OUT ? (v[k] > 0.f ? v[k] : expm1f(v[k])) : elu_bf(v[k]);
   } else if (act == DVIE_ACT_TANH) {
-    for (int k = 0; k < n; ++k) v[k] = tanh_bf(v[k]);
+    for (int k = 0; k < n; ++k) v[k] = F32OUT ? tanhf(v[k]) : tanh_bf(v[k]);
   }
 }
 
@@ -453,7 +456,7 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
                 w[4 + e] += r1[e];
               }
             }
-            act_apply(w, 8, p.act, p.alpha);
+            act_apply<true>(w, 8, p.act, p.alpha);
             if (p.dact) {
               float z[8];
               const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
@@ -625,7 +628,7 @@ __device__ __forceinline__ void ws_epilogue(const dvie_conv_desc& p, const f32x1
           w[4 + e] += r1[e];
         }
       }
-      act_apply(w, 8, p.act, p.alpha);
+      act_apply<true>(w, 8, p.act, p.alpha);
       if (p.dact) {
         const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
 #pragma unroll

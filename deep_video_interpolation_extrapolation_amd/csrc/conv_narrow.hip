@@ -248,7 +248,8 @@ __global__ __launch_bounds__(512) void conv_narrow_kernel(const dvie_conv_desc p
               w[4 + e] += r1[e];
             }
           }
-          narrow_act(w, p.act, p.alpha);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) w[k] = act_f32(w[k], p.act, p.alpha);
           if (p.dact) {
             const i32x4 tz = *(const i32x4*)((const bf16_t*)p.z + pix * p.z_ld + co);
 #pragma unroll

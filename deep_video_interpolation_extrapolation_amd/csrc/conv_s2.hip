@@ -371,7 +371,7 @@ bool conv_s2_launch(const dvie_conv_desc& p, hipStream_t s) {
     return false;
   if (p.osy != 1 || p.osx != 1 || p.ory != 0 || p.orx != 0 || p.yh != p.oh || p.yw != p.ow) return false;
   if (p.c % 16 != 0 || p.cout % 8 != 0 || p.kpad < 9 * p.c) return false;
-  if ((p.res && p.res_ld % 8 != 0) || p.y_ld % 8 != 0 || p.x_ld % 8 != 0) return false;
+  if ((p.res && (p.res_ld % 8 != 0 || ((uintptr_t)p.res & 15) != 0)) || p.y_ld % 8 != 0 || p.x_ld % 8 != 0) return false;
   const unsigned long long pix = (unsigned long long)p.n * p.ih * p.iw;
   if (((pix - 1) * (unsigned long long)p.x_ld + (unsigned long long)p.c) * 2ull >= 0xFFFFFF00ull) return false;
   if ((unsigned long long)p.cout * p.kpad * 2ull >= 0xFFFFFF00ull) return false;

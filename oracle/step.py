@@ -136,8 +136,11 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
     the new u / v (post power iteration, post Adam) are in the new disc params.
     grad_override: {"g" / "f" / "v": {name: (flat indices, values)}} written into those gradients
     before the optimizers (test support: a check against a fixture starts its next step from the
-    fixture's own signs of near-zero gradient elements, which a first Adamax / Adam step turns into
-    +-lr moves whatever their size)."""
+    fixture's own values of near-zero gradient elements: a first Adamax step moves an element by
+    lr * g / (|g| + eps), so for |g| ~ eps the move follows g's rounding-level value, not just its
+    sign); the returned gradients are this run's own (before the override), and
+    state["override_stats"] says per tensor how many elements were listed, how many changed
+    sign, and the largest own |value| among them relative to the tensor's max |gradient|."""
     from . import disc as D
     from . import vaehrnet as V
     P = {k: v.detach().clone().to(dtype).requires_grad_(True) for k, v in params.items()}
@@ -180,10 +183,22 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
         loss = loss + torch.mean(v)
     ld["loss_all"] = loss
     loss.backward()
+    st = state or {}
+    # the listed elements take the given values; st["override_stats"][tag][name] = (elements
+    # listed, elements whose sign the override changed, max |own value| / max |gradient|) and
+    # the gradients returned are this run's own, from before the override
+    own = {tag: {k: v.grad.detach().clone() for k, v in Pd.items() if v.grad is not None}
+           for tag, Pd in (("g", P), ("f", Pf), ("v", Pv))}
+    stats = {}
     for tag, Pd in (("g", P), ("f", Pf), ("v", Pv)):
         for name, (idx, vals) in (grad_override or {}).get(tag, {}).items():
-            Pd[name].grad.view(-1)[idx] = vals.to(Pd[name].grad.dtype)
-    st = state or {}
+            g = Pd[name].grad.view(-1)
+            v = vals.to(g.dtype)
+            mine = g[idx]
+            stats.setdefault(tag, {})[name] = (int(idx.numel()), int((torch.sign(mine) != torch.sign(v)).sum()),
+                                               float(mine.abs().max() / g.abs().max().clamp_min(1e-300)))
+            g[idx] = v
+    st["override_stats"] = stats
 
     def cur(src, Pd):  # u / v as the power iterations left them
         return {k: (Pd[k].detach().to(src[k].dtype) if _sn_uv(k) else src[k]) for k in src}
@@ -196,8 +211,7 @@ def gan_step(params, frame_p, video_p, vgg_state, data, frame_stats, video_stats
     newf, st["f"] = adam_fn(cur(frame_p, Pf), grads_of(Pf, frame_p), disc_lr, st.get("f"))
     newv, st["v"] = adam_fn(cur(video_p, Pv), grads_of(Pv, video_p), disc_lr, st.get("v"))
     st["stats"] = (frame_stats, video_stats) + ((vae_stats,) if vae is not None else ())
-    grads = {"g": {k: v.grad for k, v in P.items()}, "f": {k: v.grad for k, v in Pf.items() if v.grad is not None},
-             "v": {k: v.grad for k, v in Pv.items() if v.grad is not None}}
+    grads = own
     return OrderedDict((k, float(v.detach())) for k, v in ld.items()), new, newf, newv, st, grads
 
 

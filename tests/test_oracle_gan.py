@@ -125,6 +125,10 @@ def test_gan_vae_sn_two_steps_match_reference(monkeypatch):
 # * from step 2 on, the running means of those BatchNorms (they average the biases' +-lr moves);
 # * and no tensor, but step 1's near-zero gradient elements are set to the reference's values
 #   before the optimizers (below): without that the same check gives 2.1e-6 / 6.4e-6 at step 2.
+#   Adamax's first step moves an element by lr * g / (|g| + 1e-8), so for |g| ~ 1e-8 the move
+#   follows the element's rounding-level value, not only its sign (measured: 9,132 listed
+#   generator elements, none of them with the other sign, and the bar still needs them); the
+#   override's size and reach are asserted below.
 G14D_BAR = 1e-6
 
 
@@ -173,6 +177,20 @@ def test_gan_vae_sn_two_steps_match_reference_float64_per_tensor(monkeypatch):
                                                    state=state, adam="torch2", dtype=torch.float64,
                                                    grad_override=override if k == 0 else None)
         vae_stats = state["stats"][2]
+        if k == 0:
+            # the override is recorded and bounded: it touches only elements that are near zero
+            # in this run's OWN gradient (<= 2e-5 of the tensor's max, against the fixture's
+            # 1e-5 selection), at most 1 % of any tensor (measured worst 0.27 %), and changes the sign of at most a
+            # few; the step-1 gradients compared below are this run's own (before the override)
+            ost = state.pop("override_stats")
+            tot = {t: (sum(v[0] for v in d.values()), sum(v[1] for v in d.values())) for t, d in ost.items()}
+            print(f"G14d step-1 override (listed, sign changed) per model: {tot}")
+            for tag, d in ost.items():
+                Pd = {"g": Pg, "f": Pf, "v": Pv}[tag]
+                for name, (n_l, n_flip, rel) in d.items():
+                    assert rel <= 2e-5, (tag, name, rel)
+                    assert n_l <= max(16, 1e-2 * Pd[name].numel()), (tag, name, n_l)
+            assert sum(t[1] for t in tot.values()) <= 32, tot
         loss_err = np.abs(np.array(list(ld.values())) - f[t + "loss_values"]) / np.abs(f[t + "loss_values"])
         worst[t + "loss"] = (float(loss_err.max()), str(f[t + "loss_names"][int(loss_err.argmax())]), float(np.median(loss_err)))
         skip = set(bn) | ({f"{b.rsplit('.', 2)[0]}.{int(b.rsplit('.', 2)[1]) + 1}.running_mean" for b in bn}

@@ -15,7 +15,7 @@ from oracle import hrnet as O
 from plan_ref import Executor, Memory, rel_l2, track
 
 
-def _setup(monkeypatch, prec):
+def _setup(monkeypatch, prec, ex_cls=None):
     """the interpreter as the plans' executor on the CPU"""
     from deep_video_interpolation_extrapolation_amd import _lib as L
     from deep_video_interpolation_extrapolation_amd import engine as E
@@ -24,14 +24,14 @@ def _setup(monkeypatch, prec):
     monkeypatch.setattr(L, "stream_ptr", lambda *a: 0)
     mem = Memory(torch.device("cpu"))
     track(mem, monkeypatch.setattr)
-    ex = Executor(mem)
+    ex = (ex_cls or Executor)(mem)
     monkeypatch.setattr(E, "OP_HOOK", ex)
     return ex
 
 
-def _run(monkeypatch, prec, H=32, W=64):
+def _run(monkeypatch, prec, H=32, W=64, ex_cls=None):
     from deep_video_interpolation_extrapolation_amd import nets
-    ex = _setup(monkeypatch, prec)
+    ex = _setup(monkeypatch, prec, ex_cls)
     torch.manual_seed(1024)
     m = nets.InterNet(types.SimpleNamespace(syn_type="inter", highres_large=False, coarse_model="HRNet"))
     x, seg = inputs.hrnet_input(2, H, W)
@@ -109,3 +109,108 @@ def test_interpreter_runs_the_vgg_loss_plan(monkeypatch):
     e = rel_l2(a.grad, ad.grad)
     print(f"VGG loss plan: value {float(loss):.6f} vs {float(ref):.6f}, input gradient rel L2 {e:.2e}")
     assert e <= 1e-5
+
+
+class _FusedBwdCheck(Executor):
+    """The interpreter as executor, plus an INDEPENDENT float64 evaluation of the two
+    descriptors only the bf16 plan emits (OP_HEAD3_BWD, OP_SEGENC_BWD): torch autograd's
+    conv2d input / weight gradients over the OIHW parameters (reference nets/HRNet.py:
+    rgb_layer l.410-442, seg_encoder l.358-364), on the very bf16 operands the descriptor
+    reads.  It shares nothing with the interpreter's packed-weight / tap-order arithmetic, so a
+    misread tap flip or channel map in either descriptor shows as a per-tensor mismatch."""
+
+    def __init__(self, mem):
+        super().__init__(mem)
+        self.expect = {}  # parameter name -> float64 gradient (summed over the descriptors)
+        self.dh = []  # (written dh view, float64 expectation)
+
+    def _nchw(self, ptr, n, h, w, ld, c):
+        from plan_ref import nhwc
+        return self.mem.view(ptr, *nhwc(n, h, w, ld, c), torch.bfloat16).double().permute(0, 3, 1, 2)
+
+    def _add(self, name, v):
+        self.expect[name] = self.expect.get(name, 0) + v
+
+    def _unpack(self, lay, xp):
+        """packed input channels -> the layer's source channels (its cmap)"""
+        x = torch.zeros((xp.shape[0], lay.cin) + tuple(xp.shape[2:]), dtype=xp.dtype)
+        for j, ci in enumerate(lay.cmap):
+            if 0 <= ci < lay.cin:
+                x[:, ci] = xp[:, j]
+        return x
+
+    def __call__(self, plan, arr, i, meta, run):
+        from deep_video_interpolation_extrapolation_amd import _lib as L
+        from torch.nn.grad import conv2d_input, conv2d_weight
+        o = arr[i]
+        lays = {lay.name: lay for lay in plan.g.layers}
+        post = None
+        if o.kind == L.OP_HEAD3_BWD:
+            d = o.u.head3
+            lay = lays[meta["name"].split("+")[0]]
+            W = lay.m.weight.detach().to(torch.bfloat16).double()
+            pad = lay.m.padding
+            hp = self._nchw(d.h, d.n, d.hgt, d.wid, d.h_ld, d.c)
+            h = self._unpack(lay, hp)
+            g = self._nchw(d.g, d.n, d.hgt, d.wid, d.g_ld, d.cout)[:, :lay.cout]
+            self._add(lay.name + ".weight", conv2d_weight(h, W.shape, g, padding=pad))
+            dx = conv2d_input(h.shape, W, g, padding=pad)
+            dhp = torch.zeros_like(hp)
+            for j, ci in enumerate(lay.cmap):
+                if 0 <= ci < lay.cin:
+                    dhp[:, j] = dx[:, ci]
+            if d.dact:  # LeakyReLU derivative from the stored activation's sign
+                dhp = dhp * torch.where(hp > 0, 1.0, d.alpha)
+            post = (d, dhp.permute(0, 2, 3, 1))
+        elif o.kind == L.OP_SEGENC_BWD:
+            d = o.u.segenc_bwd
+            n, h, w = d.n, d.h, d.w
+            l0, l2, l4 = lays["seg_encoder.0"], lays["seg_encoder.2"], lays["seg_encoder.4"]
+            W4 = l4.m.weight.detach().to(torch.bfloat16).double()
+            W2 = l2.m.weight.detach().to(torch.bfloat16).double()
+            e2 = self._nchw(d.e2, n, h, w, d.e2_ld, 32)
+            e1 = self._nchw(d.e1, n, h, w, d.e1_ld, 32)
+            inp = self._unpack(l0, self._nchw(d.inp, n, h, w, d.in_ld, l0.cin_p))
+            dout = self._nchw(d.dout, n, h, w, d.dout_ld, 8)[:, :l4.cout]
+
+            def elu_d(e):  # ELU(1)' from its output value
+                return torch.where(e > 0, 1.0, e + 1.0)
+
+            def bf(v):  # d_e2 / d_e1 are rounded to bf16 on chip
+                return v.to(torch.bfloat16).double()
+
+            de2 = bf(conv2d_input(e2.shape, W4, dout, padding=1) * elu_d(e2))
+            de1 = bf(conv2d_input(e1.shape, W2, de2, padding=1) * elu_d(e1))
+            for lay, x, gg in ((l4, e2, dout), (l2, e1, de2), (l0, inp, de1)):
+                self._add(lay.name + ".weight", conv2d_weight(x, lay.m.weight.shape, gg, padding=1))
+                self._add(lay.name + ".bias", gg.sum((0, 2, 3)))
+        super().__call__(plan, arr, i, meta, run)
+        if post is not None:
+            d, v = post
+            self.dh.append((self.mem.view(d.dh, *__import__("plan_ref").nhwc(d.n, d.hgt, d.wid, d.dh_ld, d.c),
+                                          torch.bfloat16).double(), v))
+
+
+def test_bf16_fused_backward_descriptors_per_tensor(monkeypatch):
+    """Verdict r05 item 7: the parameter gradients the bf16-only fused descriptors produce
+    (rgb_layer.2 through OP_HEAD3_BWD; seg_encoder.0/2/4 through two OP_SEGENC_BWD, one per
+    segmentation map, summed by their slab reductions) each gated PER TENSOR against the
+    independent float64 autograd evaluation above, at <= 1e-5 relative L2 (fp32 slab sums of
+    float64 products), and the head's data gradient at the bf16 output-rounding bar."""
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    m, x, seg, w1, w2, rgb, s, ex = _run(monkeypatch, "bf16", ex_cls=_FusedBwdCheck)
+    assert ex.kinds.get(L.OP_HEAD3_BWD, 0) == 1 and ex.kinds.get(L.OP_SEGENC_BWD, 0) == 2
+    named = dict(m.coarse_model.named_parameters())
+    want = {"rgb_layer.2.weight"} | {f"seg_encoder.{k}.{p}" for k in (0, 2, 4) for p in ("weight", "bias")}
+    assert want <= set(ex.expect), sorted(ex.expect)
+    # the head's bias gradient comes from its own column-sum op (interpreted generically)
+    errs = {k: rel_l2(named[k].grad, ex.expect[k]) for k in sorted(ex.expect)}
+    for k, e in errs.items():
+        print(f"  {k:24s} rel L2 {e:.2e}")
+    bad = {k: e for k, e in errs.items() if not e <= 1e-5}
+    assert not bad, bad
+    assert len(ex.dh) == 1
+    got, ref = ex.dh[0]
+    e = rel_l2(got, ref)
+    print(f"  rgb_layer.2 dh (bf16)     rel L2 {e:.2e}")
+    assert e <= 4e-3

@@ -6,6 +6,8 @@ set -o pipefail
 la=$1; lb=$2; tag=${3:-ab_lib}
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/$tag
 pkg=deep_video_interpolation_extrapolation_amd/libdvie.so
+cp $pkg gpurun_out/$tag/orig.so
+trap 'cp gpurun_out/$tag/orig.so $pkg' EXIT  # the package library is restored however the script ends
 for r in 1 2; do
   for v in a b; do
     if [ $v = a ]; then cp "$la" $pkg; else cp "$lb" $pkg; fi
@@ -14,4 +16,3 @@ for r in 1 2; do
     echo "lib $v ($(basename $([ $v = a ] && echo $la || echo $lb))) run $r $(grep -o '"value": [0-9.]*' gpurun_out/$tag/b_${v}_$r.json)"
   done
 done
-cp "$la" $pkg

@@ -7,6 +7,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/$tag; mkdir -p $out
 pkg=deep_video_interpolation_extrapolation_amd/libdvie.so
 cp $pkg $out/orig.so
+# restore the package library however the script ends (outer timeout / SIGKILL of a child included)
+trap 'cp $out/orig.so $pkg' EXIT
 for v in a b a b; do
   lib=$([ $v = a ] && echo $la || echo $lb)
   cp "$lib" $pkg
