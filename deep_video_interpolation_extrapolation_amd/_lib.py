@@ -41,7 +41,7 @@ class ConvDesc(ctypes.Structure):
         ("th", i32), ("tw", i32), ("dy0", i32), ("dx0", i32), ("ddy", i32), ("ddx", i32),
         ("yh", i32), ("yw", i32), ("osy", i32), ("osx", i32), ("ory", i32), ("orx", i32),
         ("act", i32), ("dact", i32), ("beta", i32), ("dtype", i32),
-        ("out_f32", i32), ("alpha", f32),
+        ("out_f32", i32), ("alpha", f32), ("phc", i32), ("pad1", i32),
     ]
 
 
@@ -53,7 +53,7 @@ class WgradDesc(ctypes.Structure):
         ("ih", i32), ("iw", i32), ("c", i32), ("sy", i32),
         ("sx", i32), ("th", i32), ("tw", i32), ("dy0", i32),
         ("dx0", i32), ("ddy", i32), ("ddx", i32), ("splits", i32),
-        ("dtype", i32), ("pad0", i32), ("bws", vp),
+        ("dtype", i32), ("tmap", i32), ("bws", vp), ("ws_taps", i32), ("pad1", i32),
     ]
 
 

@@ -581,6 +581,8 @@ int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (d->bws) DVIE_CHECK_ARG(d->cout % 4 == 0 && d->cout <= 4096 && d->g_ld % 4 == 0, "wgrad: bias partials (cout=%d)", d->cout);
   if (wgrad_halo_launch(*d, s)) DVIE_RETURN_LAUNCH();  // (bias sums fused when bws is set)
+  DVIE_CHECK_ARG(d->ws_taps == 0, "wgrad: a shared-slab phase launch (ws_taps=%d) needs the halo kernel "
+                 "(bf16, stride 1 over the phase view, ow %% 64 == 0)", d->ws_taps);
   if (d->dtype == DVIE_BF16)
     DVIE_LAUNCH(wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, *d, chunk);
   else

@@ -361,6 +361,7 @@ static void dispatch_conv(const dvie_conv_desc& p, hipStream_t s) {
 }
 
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_halo.hip
+bool conv_halo_ph4_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_halo.hip
 bool conv1x1_launch(const dvie_conv_desc& p, hipStream_t s);    // conv1x1.hip
 bool conv_s2_launch(const dvie_conv_desc& p, hipStream_t s);    // conv_s2.hip
 
@@ -404,6 +405,11 @@ extern "C" int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream) {
     c.y = (char*)d->y + n0 * img_y * d->y_ld * oes;
     if (d->res) c.res = (const char*)d->res + n0 * img_y * d->res_ld * oes;
     if (d->z) c.z = (const char*)d->z + n0 * img_y * d->z_ld * es;
+    if (c.phc) {  // the one-launch stride-2 data gradient: the halo kernel only
+      DVIE_CHECK_ARG(conv_halo_ph4_launch(c, s), "conv: phase-split output (phc=%d) needs bf16, 2x2 taps at "
+                     "(0,0), osy=osx=2, cout=4*phc, phc %% 32 == 0, no bias", c.phc);
+      continue;
+    }
     if (conv1x1_launch(c, s)) continue;
     if (conv_halo_launch(c, s)) continue;
     if (conv_s2_launch(c, s)) continue;

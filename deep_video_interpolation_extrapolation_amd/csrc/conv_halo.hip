@@ -131,11 +131,20 @@ struct JobInfo {
   int valid, t, k, c0, n, y0, x0;
 };
 
-template <int TM, int WC, int WP, int TH, int TW, bool OUTF32>
+// PH4 (TH = TW = 2, include/dvie.h dvie_conv_desc.phc): the stride-2 data gradient's four
+// output phases in one launch.  Output channel block q of phc channels is phase (a, b) =
+// ph4_a/b(q); it is placed at (2 oy + a, 2 ox + b) and uses tap (i, j) only if (i == 0 || a)
+// and (j == 0 || b), so an accumulator block skips the MFMAs of the taps its phase lacks
+// (9 of the 16 tap-phase products are nonzero).
+__host__ __device__ constexpr int ph4_a(int q) { return q == 1 || q == 3; }
+__host__ __device__ constexpr int ph4_b(int q) { return q == 1 || q == 2; }
+
+template <int TM, int WC, int WP, int TH, int TW, bool OUTF32, bool PH4 = false>
 __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_desc p, int n_ct, int n_tiles,
                                                                  int tiles_x, int tiles_y, int persistent,
                                                                  int epi_pre) {
   typedef HaloCfg<TM, WC, WP, TH, TW> C;
+  static_assert(!PH4 || (TH == 2 && TW == 2 && !OUTF32), "phase-split output: 2 x 2 taps, bf16");
   constexpr int NW = C::NW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
 
@@ -285,9 +294,15 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
 #pragma unroll
         for (int P = 0; P < 2; ++P) {
           const int ox = Jt.x0 + 32 * b + r32;
-          const int co = Jt.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh;
-          const bool ok = oy < p.oh && ox < p.ow && co < p.cout;
-          const long long dp = (long long)wp * p.osy * p.yw + (long long)(32 * b + r32) * p.osx;
+          int co = Jt.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh;
+          bool ok = oy < p.oh && ox < p.ow && co < p.cout;
+          long long dp = (long long)wp * p.osy * p.yw + (long long)(32 * b + r32) * p.osx;
+          if constexpr (PH4) {  // phase (a, pb) of this block: placement offset, channel within the phase
+            const int q = (Jt.c0 + wc * 32 * TM + 32 * i) / p.phc, a = ph4_a(q), pb = ph4_b(q);
+            dp += (long long)a * p.yw + pb;
+            co -= q * p.phc;
+            ok = ok && 2 * oy + a < p.yh && 2 * ox + pb < p.yw;
+          }
           const unsigned OFF = 0xFFFFFFF0u;
           if (p.res)
             pre_r[i][b][P] = __builtin_amdgcn_raw_buffer_load_b128(rr, ok ? (unsigned)((dp * p.res_ld + co) * 2) : OFF, 0, 0);
@@ -334,6 +349,14 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
     }
     if (!J.valid) break;
     const int hb = j % C::NH;
+    int tuse[TM];  // PH4: taps (bit t = i*2 + j) accumulator block i multiplies
+    if constexpr (PH4) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int q = (J.c0 + wc * 32 * TM + 32 * i) / p.phc;
+        tuse[i] = 1 | (ph4_b(q) ? 2 : 0) | (ph4_a(q) ? 4 : 0) | (ph4_a(q) && ph4_b(q) ? 8 : 0);
+      }
+    }
     if (J.k == 0) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -377,12 +400,16 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
         __builtin_amdgcn_sched_barrier(0);
         const int fb = s & 1;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (PH4) {
+            if (!((tuse[i] >> t) & 1)) continue;  // (wave-uniform)
+          }
 #pragma unroll
           for (int b = 0; b < 2; ++b)
             acc[i][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[fb][i]),
                                                                 __builtin_bit_cast(bf16x8, bfr[fb][b]), acc[i][b], 0,
                                                                 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       // everything issued before this step has landed (this step's loads may stay in flight;
@@ -423,11 +450,18 @@ __global__ __launch_bounds__(WC* WP * 64) void conv_halo_kernel(const dvie_conv_
         const int oy = J.y0 + wp, ox = J.x0 + 32 * b + r32;
         if (oy >= p.oh || ox >= p.ow) continue;
         // output placement (identity, or a stride phase of the strided data gradient)
-        const long long pix = ((long long)J.n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+        long long pix = ((long long)J.n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+        int cq = 0;  // PH4: first channel of this block's phase
+        if constexpr (PH4) {
+          const int q = (J.c0 + wc * 32 * TM + 32 * i) / p.phc, a = ph4_a(q), pb = ph4_b(q);
+          if (2 * oy + a >= p.yh || 2 * ox + pb >= p.yw) continue;
+          pix += (long long)a * p.yw + pb;
+          cq = q * p.phc;
+        }
 #pragma unroll
         for (int P = 0; P < 2; ++P) {
-          const int co = J.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh;
-          if (co >= p.cout) continue;
+          const int co = J.c0 + wc * 32 * TM + 32 * i + 16 * P + 8 * hh - cq;
+          if (co + cq >= p.cout) continue;
           float* w = v[P];
           if (p.bias) {
             const f32x4 b0 = *(const f32x4*)(p.bias + co), b1 = *(const f32x4*)(p.bias + co + 4);
@@ -522,7 +556,7 @@ static int halo_wait_flag() {
 #endif
 }
 
-template <int TM, int WC, int WP, int TH, int TW>
+template <int TM, int WC, int WP, int TH, int TW, bool PH4 = false>
 static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
   typedef HaloCfg<TM, WC, WP, TH, TW> C;
   if constexpr (C::SMEM > 163840) {
@@ -537,7 +571,10 @@ static bool try_halo(const dvie_conv_desc& p, hipStream_t s) {
     const int cap = 256 * (per_cu > 2 ? 2 : per_cu);
     const int persistent = n_tiles > cap ? 1 : 0;
     const int grid = persistent ? cap : n_tiles;
-    if (p.out_f32)
+    if constexpr (PH4)
+      DVIE_LAUNCH((conv_halo_kernel<TM, WC, WP, TH, TW, false, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
+                  n_tiles, tiles_x, tiles_y, persistent, (epi_prefetch_on ? 1 : 0) | halo_setprio | halo_wait_flag());
+    else if (p.out_f32)
       DVIE_LAUNCH((conv_halo_kernel<TM, WC, WP, TH, TW, true>), dim3(grid), dim3(C::NTH), 0, s, p, n_ct,
                          n_tiles, tiles_x, tiles_y, persistent, halo_setprio | halo_wait_flag());
     else
@@ -1664,6 +1701,28 @@ static bool conv_h8_launch(const dvie_conv_desc& p, hipStream_t s) {
 static const bool nk_env_off = getenv("DVIE_CONV_NK") && *getenv("DVIE_CONV_NK") == '0';
 
 bool conv_narrow_launch(const dvie_conv_desc& p, hipStream_t s);  // conv_narrow.hip
+
+// DVIE_PH4_CFG: tile configuration of the one-launch stride-2 data gradient (3 = 64 channels
+// x 4 rows, 4 = 128 x 4; A/B runs)
+static int ph4_cfg(const dvie_conv_desc& p) {
+  const char* e = getenv("DVIE_PH4_CFG");
+  if (e && *e) return atoi(e);
+  return p.cout % 128 == 0 ? 4 : 3;
+}
+
+// The stride-2 data gradient's four phases in one launch (dvie_conv_desc.phc > 0); false:
+// the descriptor does not meet the kernel's conditions (the caller reports it).
+bool conv_halo_ph4_launch(const dvie_conv_desc& p, hipStream_t s) {
+  if (p.dtype != DVIE_BF16 || p.out_f32 || p.bias || p.phc <= 0 || p.phc % 32 != 0 || p.cout != 4 * p.phc) return false;
+  if (p.th != 2 || p.tw != 2 || p.dy0 != 0 || p.dx0 != 0 || p.ddy != 1 || p.ddx != 1 || p.sy != 1 || p.sx != 1)
+    return false;
+  if (p.osy != 2 || p.osx != 2 || p.ory != 0 || p.orx != 0) return false;
+  if (p.c % 64 != 0 && p.c > 64) return false;
+  const unsigned long long pix = (unsigned long long)p.n * p.ih * p.iw;
+  if (pix >= (1ull << 31) || ((pix - 1) * (unsigned long long)p.x_ld + (unsigned long long)p.c) * 2ull >= 0xFFFFFF00ull)
+    return false;
+  return ph4_cfg(p) == 3 ? try_halo<1, 2, 4, 2, 2, true>(p, s) : try_halo<2, 2, 4, 2, 2, true>(p, s);
+}
 
 // Returns true when the halo kernel took the launch.
 bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {

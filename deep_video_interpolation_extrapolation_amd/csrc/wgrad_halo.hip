@@ -429,7 +429,9 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
   // the taps its partner owns (lane-fastest, conflict-free), one barrier, and adds the parked
   // values to its own taps as it stores them -- both halves store, behind a single barrier.
   // C layout: column (ci) = lane & 31, rows (co) = 8*(e>>2) + 4*(lane>>5) + (e&3)
-  const long long ws_k = (long long)C::NT * p.c;
+  // slab rows: NT * c values, or ws_taps * c of which this launch fills its taps' column
+  // blocks (p.tmap; the stride-2 weight gradient's four phase launches share one slab set)
+  const long long ws_k = (long long)(p.ws_taps > 0 ? p.ws_taps : C::NT) * p.c;
   const int r32 = lane & 31, hh = lane >> 5;
   float* slab = p.ws + (long long)(merge ? split : 2 * split + wrow) * p.cout * ws_k;
   constexpr int TO = (C::NT + 1) / 2;  // taps [0, TO) are row half 0's, [TO, NT) row half 1's
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
         for (int e = 0; e < 16; ++e) {
           const int co = c0 + wco * 32 * TMO + 32 * jo + 8 * (e >> 2) + 4 * hh + (e & 3);
           if (co < p.cout && (!(dbg & 32) || acc[t * TMO * TMI + j][e] == 12345.678f))
-            slab[(long long)co * ws_k + (long long)t * p.c + ci] =
+            slab[(long long)co * ws_k + (long long)(p.ws_taps > 0 ? (p.tmap >> (4 * t)) & 15 : t) * p.c + ci] =
                 acc[t * TMO * TMI + j][e] + (merge ? X[t * PSZ + (j * 16 + e) * 64] : 0.f);
         }
       }
@@ -628,7 +630,8 @@ static bool wgrad_halo_eligible(const dvie_wgrad_desc& p) {
   if (p.dtype != DVIE_BF16) return false;
   if (wg_halo_env_off) return false;
   if (p.sy != 1 || p.sx != 1 || p.ddy != 1 || p.ddx != 1) return false;
-  if (!((p.th == 1 && p.tw == 1) || (p.th == 3 && p.tw == 3))) return false;
+  if (!((p.th == 1 && p.tw == 1) || (p.th == 3 && p.tw == 3) || (p.th <= 2 && p.tw <= 2))) return false;
+  if (p.ws_taps > 0 && (p.ws_taps > 16 || p.th * p.tw > 4)) return false;
   if (p.c % 8 != 0 || p.cout % 8 != 0) return false;
   if (p.g_ld % 8 != 0 || p.x_ld % 8 != 0) return false;
   const unsigned long long npx = (unsigned long long)p.n * p.ih * p.iw, npg = (unsigned long long)p.n * p.oh * p.ow;
@@ -652,8 +655,9 @@ static const bool wg_narrow_env_off = getenv("DVIE_WG_NARROW") && *getenv("DVIE_
 static const bool wg_wide_env_off = getenv("DVIE_WG_WIDE") && *getenv("DVIE_WG_WIDE") == '0';
 
 static WgPlan wgrad_plan(const dvie_wgrad_desc& p) {
-  if (p.th == 3) return {4, 1, 1, 0};
-  if (!wg_wide_env_off && p.c > 128 && p.cout > 128 && p.dy0 == 0 && p.dx0 == 0 && p.oh == p.ih && p.ow == p.iw)
+  // (the phase launches of one shared slab set all take this plan: equal tiles and splits)
+  if (p.th > 1 || p.tw > 1 || p.ws_taps > 0) return {4, 1, 1, 0};
+  if (!wg_wide_env_off && p.ws_taps == 0 && p.c > 128 && p.cout > 128 && p.dy0 == 0 && p.dx0 == 0 && p.oh == p.ih && p.ow == p.iw)
     return {1, 4, 4, 1};
   const char* e = getenv("DVIE_WG_TM");  // tuning override for 1x1: "<tmo><tmi>", e.g. "11"
   if (e && e[0] && e[1]) return {2, e[0] == '2' ? 2 : 1, e[1] == '2' ? 2 : 1, 0};
@@ -753,6 +757,16 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
   if (p.th == 3 && p.cout > 32 && wg_pipe)
     DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
+  // the stride-2 weight gradient's phase launches (ws_taps): 2 x 2, 2 x 1, 1 x 2 tap grids
+#define DVIE_WG2(TH, TW)                                                                                        \
+  else if (p.th == TH && p.tw == TW)                                                                            \
+    DVIE_LAUNCH((wgrad_halo_kernel<TH, TW, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
+                tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
+  DVIE_WG2(2, 2) DVIE_WG2(2, 1) DVIE_WG2(1, 2)
+  else if (p.ws_taps > 0 && p.th == 1 && p.tw == 1)
+    DVIE_LAUNCH((wgrad_halo_kernel<1, 1, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
+                tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
+#undef DVIE_WG2
   else if (p.th == 3 && p.cout <= 32 && !wg_narrow_env_off)
     DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 4, true>), dim3(grid), dim3(256), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);

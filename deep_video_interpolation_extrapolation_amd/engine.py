@@ -693,6 +693,7 @@ class Plan:
                 d.cout_s, d.cin_s, d.kh_s, d.kw_s, d.dtype = nbias, 1, 1, 1, L.F32
                 descs.append(d)
             lay.wd = []
+            lay.wd4 = None  # (the one-launch stride-2 data-gradient weights: packed by this plan)
         self._pack_descs = descs  # dgrad packs appended during backward build
 
     def _pack_desc(self, lay, dst, rows, kpad, c, mode, taps, cmap_t):
@@ -720,6 +721,38 @@ class Plan:
             out.append((ph, t, kpad))
         lay.wd.append((key, out))
         return out
+
+    # phase order of the one-launch stride-2 data gradient (include/dvie.h dvie_conv_desc.phc)
+    PH4_ORDER = ((0, 0), (1, 1), (0, 1), (1, 0))
+
+    def _ph4_eligible(self, lay, x):
+        """stride-2 3x3 pad-1 data gradient as ONE launch of the halo kernel with the four
+        output phases as channel blocks (bf16; DVIE_PH4=0 keeps the four phase launches)"""
+        # phc <= 128: at 256 output channels per phase (transition1.1, 256 -> 128) the four
+        # launches measured faster (0.369 vs 0.532 ms/step: each 128-channel tile of the one
+        # launch streams the weight rows of all four taps, 7 of 16 of them zero for its phase,
+        # and re-stages the dy halo for each of the 8 channel blocks); the 64- / 128-channel
+        # layers gain 0.175 ms/step together (profiles/r06d/)
+        return (self.dtype == torch.bfloat16 and os.environ.get("DVIE_PH4", "1") != "0" and lay.stride == 2
+                and lay.kh == 3 and lay.kw == 3 and lay.pad == 1 and lay.dil == 1 and not lay.transposed
+                and x.c == lay.cin_p and lay.cin_p % 32 == 0 and lay.cin_p <= 128
+                and (lay.cout_p % 64 == 0 or lay.cout_p < 64))
+
+    def _dgrad_weights_ph4(self, lay):
+        """packed [4 * cin_p][kpad] weights of the one-launch stride-2 data gradient: row block
+        q = phase (a, b) = PH4_ORDER[q], tap (i, j) of the 2 x 2 grid = forward weight
+        (kh, kw) = (a + 1 - 2i, b + 1 - 2j) (zero where that is outside the kernel)"""
+        if getattr(lay, "wd4", None) is not None:
+            return lay.wd4
+        kpad = rup(4 * lay.cout_p, 64)
+        t = torch.zeros((4 * lay.cin_p, kpad), dtype=self.dtype, device=self.device)
+        self.keep.append(t)
+        for q, (a, b) in enumerate(self.PH4_ORDER):
+            taps = dict(th=2, tw=2, kh0=a + 1, kw0=b + 1, dkh=-2, dkw=-2)
+            self._pack_descs.append(self._pack_desc(lay, t[q * lay.cin_p:(q + 1) * lay.cin_p], lay.cin_p, kpad,
+                                                    lay.cout_p, 1, taps, lay.cmap_t))
+        lay.wd4 = (t, kpad)
+        return lay.wd4
 
     # ---------------- descriptor factories ----------------
     def _op(self, kind):
@@ -1450,6 +1483,20 @@ class Plan:
                 if self._im2col_dgrad(lay, x, phases):
                     return self._im2col_dgrad_ops(lay, x, xg, out, gout, gld, phases[0], res, res_ld, z, z_ld, dact,
                                                   beta)
+                if self._ph4_eligible(lay, x):
+                    wt, kpad = self._dgrad_weights_ph4(lay)
+                    taps = dict(th=2, tw=2, dy0=0, dx0=0, ddy=1, ddx=1)
+                    o = self.conv_desc(gout, gld, nb, out.H, out.W, lay.cout_p, wt.data_ptr(), kpad, 4 * x.c, out.H,
+                                       out.W, 1, 1, taps, xg, x.buf.C, x.H, x.W, osy=2, osx=2, res=res, res_ld=res_ld,
+                                       z=z, z_ld=z_ld, dact=dact, beta=beta)
+                    o.u.conv.phc = x.c
+                    npx = nb * x.H * x.W
+                    o.meta = dict(cls="conv_dgrad", name=lay.name,
+                                  flops=2.0 * nb * out.H * out.W * lay.cin * lay.cout * 9,
+                                  bytes=float(self.es * (nb * out.H * out.W * lay.cout
+                                                         + npx * lay.cin * (1 + (res is not None) + (z is not None) + beta)
+                                                         + lay.cout * lay.cin * 9)))
+                    return [o]
                 for ph, wt, kpad in phases:
                     o = self.conv_desc(
                         gout, gld, nb, out.H, out.W, lay.cout_p, wt.data_ptr(), kpad, x.c, ph["oh"], ph["ow"], 1, 1,
@@ -1457,7 +1504,8 @@ class Plan:
                         res=res, res_ld=res_ld, z=z, z_ld=z_ld, dact=dact, beta=beta)
                     npx = nb * ph["oh"] * ph["ow"]
                     frac = npx / float(nb * x.H * x.W)
-                    o.meta = dict(cls="conv_dgrad", name=lay.name,
+                    o.meta = dict(cls="conv_dgrad",
+                                  name=lay.name + (f" [phase {ph['ry']}{ph['rx']}]" if len(phases) > 1 else ""),
                                   flops=2.0 * npx * lay.cin * lay.cout * ph["th"] * ph["tw"],
                                   bytes=float(self.es * (frac * nb * out.H * out.W * lay.cout
                                                          + npx * lay.cin * (1 + (res is not None) + (z is not None) + beta)
@@ -1467,10 +1515,103 @@ class Plan:
 
             self._contrib(x, em)
 
+    def _wgrad_s2_eligible(self, lay, x, out):
+        """stride-2 3x3 pad-1 weight gradient as its four input phases on the halo kernel
+        (include/dvie.h dvie_wgrad_desc.ws_taps; DVIE_WGRAD_S2=0 keeps the per-tap kernel,
+        DVIE_WGRAD_S2=2 takes every eligible layer).  Default: inputs of >= 256 channels
+        (transition1.1: 0.377 -> 0.297 ms/step); each phase launch streams the whole output
+        gradient, so on the 64- / 128-channel inputs the four launches measured 2-35% slower
+        than the per-tap kernel (profiles/r06e/)"""
+        mode = os.environ.get("DVIE_WGRAD_S2", "1")
+        if mode == "1" and x.c < 256:
+            return False
+        return (self.dtype == torch.bfloat16 and mode != "0" and lay.stride == 2
+                and lay.kh == 3 and lay.kw == 3 and lay.pad == 1 and lay.dil == 1 and not lay.transposed
+                and x.H % 2 == 0 and x.W % 2 == 0 and out.H == x.H // 2 and out.W == x.W // 2 and out.W % 64 == 0
+                and x.c % 8 == 0 and x.buf.C % 8 == 0)
+
+    def _emit_wgrad_s2(self, op, gout, gld):
+        """The stride-2 weight gradient as four stride-1 launches, one per input phase
+        (a, b): tap (i, j) of phase (a, b) is forward tap (kh, kw) = (1, .) for a = 0, (0 | 2, .)
+        for a = 1 (i = 0 | 1; likewise for columns), read from the phase view x[2r + a][2q + b]
+        (x + (a W + b) ld, x_ld 2 ld, iw = W as the row pitch); each launch fills its taps'
+        column blocks of one [splits][cout][9 c] slab set, reduced once."""
+        lay, x, out = op.layer, op.x, op.out
+        nb = self.nb
+        npix = nb * out.H * out.W
+        lib = L.load()
+        ops, slabs, bslabs = [], None, 0
+        for a in (0, 1):
+            for b in (0, 1):
+                o = self._op(L.OP_WGRAD)
+                d = o.u.wgrad
+                d.g, d.x, d.ws = gout, self.ptr(x) + (a * x.W + b) * x.buf.C * self.es, 0
+                d.g_ld, d.x_ld = gld, 2 * x.buf.C
+                d.n, d.oh, d.ow, d.cout = nb, out.H, out.W, lay.cout_p
+                d.ih, d.iw, d.c, d.sy, d.sx = x.H // 2, x.W, x.c, 1, 1
+                d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = 1 + a, 1 + b, -a, -b, 1, 1
+                khs, kws = ([1] if a == 0 else [0, 2]), ([1] if b == 0 else [0, 2])
+                d.tmap = sum((kh * 3 + kw) << (4 * (i * len(kws) + j)) for i, kh in enumerate(khs)
+                             for j, kw in enumerate(kws))
+                d.ws_taps = 9
+                d.dtype = self.dt
+                hint = lib.dvie_wgrad_splits_hint(ctypes.byref(d))
+                assert hint > 0, f"{lay.name}: the halo weight-gradient kernel refused a stride-2 phase launch"
+                d.splits = hint
+                n_s = lib.dvie_wgrad_slabs(ctypes.byref(d))
+                assert slabs in (None, n_s), "stride-2 phase launches disagree on their slab count"
+                slabs = n_s
+                if a == 0 and b == 0 and lay.has_bias:  # the bias column sums ride on one launch
+                    d.bws = 1
+                    bslabs = lib.dvie_wgrad_bias_slabs(ctypes.byref(d))
+                    d.bws = None
+                    o.bws_off = slabs * lay.cout_p * 9 * x.c
+                nt = len(khs) * len(kws)
+                o.meta = dict(cls="conv_wgrad", name=lay.name + f" [phase {a}{b}]",
+                              flops=2.0 * npix * lay.cout * lay.cin * nt,
+                              bytes=float(self.es * (npix * lay.cout + npix * lay.cin)
+                                          + 4 * slabs * lay.cout_p * nt * x.c))
+                ops.append(o)
+        wfl = slabs * lay.cout_p * 9 * x.c
+        self.ws_floats = max(self.ws_floats, wfl + bslabs * lay.cout_p)
+        self.bwd += ops
+        self._emit_wreduce(lay, slabs, 9 * x.c, x.c, bslabs, wfl)
+
+    def _emit_wreduce(self, lay, slabs, ws_k, c, bslabs, bias_off):
+        """the slab reductions of a weight gradient (and of its bias partials) into the .grad
+        views, and the layer's completion bookkeeping"""
+        o = self._op(L.OP_WREDUCE)
+        r = o.u.wreduce
+        r.ws, r.dw, r.cmap = 0, 0, lay.cmap_t.data_ptr()
+        r.splits, r.ws_rows, r.ws_k, r.co_off = slabs, lay.cout_p, ws_k, 0
+        r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, lay.cin, lay.kh, lay.kw, c
+        first = lay not in self.wg_first
+        r.beta = 0 if first else 1
+        o.meta = _reduce_meta(lay.name, r)
+        self.bwd.append(o)
+        self._grad_slots.append((len(self.bwd) - 1, lay, "weight", first))
+        if lay.has_bias:
+            o = self._op(L.OP_WREDUCE)
+            r = o.u.wreduce
+            r.ws, r.dw, r.cmap = 0, 0, None
+            r.splits, r.ws_rows, r.ws_k, r.co_off = bslabs, lay.cout_p, 1, 0
+            r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c = lay.cout, 1, 1, 1, 1
+            r.beta = 0 if first else 1
+            o.meta = _reduce_meta(lay.name + ".bias", r)
+            o.ws_off = bias_off
+            self.bwd.append(o)
+            self._grad_slots.append((len(self.bwd) - 1, lay, "bias", first))
+        self.wg_first[lay] = True
+        self._uses_left[lay] -= 1
+        if self._uses_left[lay] == 0:
+            self.completions.append((len(self.bwd), lay))
+
     def _emit_wgrad(self, op, gout, gld):
         """weight (and bias) gradient of a conv: split-K partial slabs + reduction into the
         OIHW .grad view, appended to the backward list (weight lane)."""
         lay, x, out = op.layer, op.x, op.out
+        if self._wgrad_s2_eligible(lay, x, out) and gld % 8 == 0:
+            return self._emit_wgrad_s2(op, gout, gld)
         nb = self.nb
         npix = nb * out.H * out.W
         taps = lay.fwd_taps()

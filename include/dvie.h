@@ -81,6 +81,16 @@ typedef struct dvie_conv_desc {
   int act, dact, beta, dtype;
   int out_f32; /* 1: y (and res) are fp32, 0: y has elem type dtype */
   float alpha; /* activation slope / parameter */
+  int phc;     /* 0, or the stride-2 data gradient of a 3x3 pad-1 conv (nets/HRNet.py:181-194,
+                  466-474) in ONE launch: cout = 4*phc output channels are the four output
+                  phases, blocks of phc channels in the order (a,b) = (0,0), (1,1), (0,1), (1,0);
+                  channel q*phc + ci of grid pixel (oy, ox) lands at channel ci of output pixel
+                  (2*oy + a, 2*ox + b) (osy = osx = 2, ory = orx = 0; pixels outside yh x yw are
+                  skipped).  Taps 2 x 2 at dy0 = dx0 = 0; tap (i, j) carries weight row
+                  kh = a + 1 - 2i, kw = b + 1 - 2j of the forward kernel, so a phase with a = 0
+                  (b = 0) has no i = 1 (j = 1) taps: those MFMAs are skipped, not multiplied by
+                  zero.  bf16, phc % 32 == 0, no bias / fp32 output. */
+  int pad1;
 } dvie_conv_desc;
 
 int dvie_conv2d_fwd(const dvie_conv_desc* d, void* stream);
@@ -101,12 +111,23 @@ typedef struct dvie_wgrad_desc {
   int ih, iw, c, sy;
   int sx, th, tw, dy0;
   int dx0, ddy, ddx, splits;
-  int dtype, pad0;
+  int dtype;
+  int tmap;   /* with ws_taps > 0: tap t of this launch's th x tw grid (t = i*tw + j) is column
+                 block (tmap >> 4t) & 15 of the slab rows */
   float* bws; /* NULL, or the bias-gradient partials: bws[slab][cout] = column sums of g over
                  the slab's pixels (dvie_wgrad_bias_slabs slabs; reduce them with
                  dvie_wgrad_reduce, ws_k = 1).  The halo weight-gradient kernels sum g while
                  they hold it for the MFMAs (no second pass over g); other launches run a
                  column-sum pass.  Replaces the separate nn.Conv2d bias backward. */
+  int ws_taps; /* 0: slab rows hold th*tw*c values, tap t at column t*c.  > 0: rows hold
+                  ws_taps*c values and this launch writes only its taps' column blocks (tmap),
+                  so several launches fill one slab set: the stride-2 weight gradient
+                  (nets/HRNet.py:181-194, 466-474) runs as its four input phases, each a
+                  stride-1 weight gradient over a phase view of x (x + (a*W + b)*ld, x_ld =
+                  2*ld, ih = H/2, iw = W as the row pitch: the halo kernels, which then read
+                  only columns < ow, require ow % 64 == 0), into the 9 tap columns of one
+                  [splits][cout][9*c] slab set reduced by one dvie_wgrad_reduce. */
+  int pad1;
 } dvie_wgrad_desc;
 
 int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream);

@@ -181,11 +181,38 @@ class Interp:
             acc += torch.einsum("nchw,oc->nhwo", patch, w[:, t * c:(t + 1) * c])
         return acc
 
+    # phase order of dvie_conv_desc.phc (include/dvie.h)
+    PH4 = ((0, 0), (1, 1), (0, 1), (1, 0))
+
     def ref_conv(self, d):
         dt = _tdt(d.dtype)
         ydt = torch.float32 if (d.out_f32 or d.dtype == L.F32) else torch.bfloat16
         v = self.conv_acc(d.x, d.x_ld, d.n, d.ih, d.iw, d.c, d.w, d.kpad, d.cout, d.oh, d.ow, d.sy, d.sx, d.th, d.tw,
                           d.dy0, d.dx0, d.ddy, d.ddx, dt)
+        if d.phc:  # one-launch stride-2 data gradient: channel block q -> output phase PH4[q]
+            assert d.cout == 4 * d.phc and not d.bias and ydt == torch.bfloat16
+            es = _es(ydt)
+            out = []
+            for q, (a, b) in enumerate(self.PH4):
+                oh = min(d.oh, (d.yh - a + 1) // 2)
+                ow = min(d.ow, (d.yw - b + 1) // 2)
+                if oh <= 0 or ow <= 0:
+                    continue
+                vq = v[:, :oh, :ow, q * d.phc:(q + 1) * d.phc]
+
+                def at(ptr, ld, a=a, b=b, oh=oh, ow=ow):
+                    return (ptr + (a * d.yw + b) * ld * es, (d.n, oh, ow, d.phc),
+                            (d.yh * d.yw * ld, 2 * d.yw * ld, 2 * ld, 1))
+                if d.res:
+                    vq = vq + self.rd(*at(d.res, d.res_ld), ydt)
+                yp, ysh, yst = at(d.y, d.y_ld)
+                if d.beta:
+                    vq = vq + self.rd(yp, ysh, yst, ydt)
+                vq = act_fwd(vq, d.act, d.alpha)
+                if d.dact:
+                    vq = vq * act_dz(self.rd(*at(d.z, d.z_ld), dt), d.dact, d.alpha)
+                out.append((f"y phase {a}{b}", yp, ysh, yst, ydt, vq, "act"))
+            return out
 
         def placed(ptr, ld, pdt):
             shape, st = nhwc(d.n, d.oh, d.ow, ld, d.cout)
@@ -207,10 +234,15 @@ class Interp:
         return [("y", yp, ysh, yst, ydt, v, "act" if ydt == torch.bfloat16 else "f32")]
 
     # ---------------- weight gradient ----------------
-    def wgrad_sum(self, g_ptr, g_ld, x_ptr, x_ld, n, oh, ow, cout, ih, iw, c, sy, sx, th, tw, dy0, dx0, ddy, ddx, dt):
-        """[cout][taps][c]: sum_pix g[pix][co] x[pix + tap][ci]"""
+    def wgrad_sum(self, g_ptr, g_ld, x_ptr, x_ld, n, oh, ow, cout, ih, iw, c, sy, sx, th, tw, dy0, dx0, ddy, ddx, dt,
+                  xw=None):
+        """[cout][taps][c]: sum_pix g[pix][co] x[pix + tap][ci]; xw: the number of valid x
+        columns when iw is only the row pitch (the stride-2 phase views)"""
         g = self.rd(g_ptr, *nhwc(n, oh, ow, g_ld, cout), dt)
-        x = self.rd(x_ptr, *nhwc(n, ih, iw, x_ld, c), dt).permute(0, 3, 1, 2)
+        if xw is None:
+            x = self.rd(x_ptr, *nhwc(n, ih, iw, x_ld, c), dt).permute(0, 3, 1, 2)
+        else:
+            x = self.rd(x_ptr, (n, ih, xw, c), (ih * iw * x_ld, iw * x_ld, x_ld, 1), dt).permute(0, 3, 1, 2)
         dys = [dy0 + i * ddy for i in range(th)]
         dxs = [dx0 + j * ddx for j in range(tw)]
         pt = self.taps_patches(x, oh, ow, sy, sx, dys, dxs)
@@ -223,10 +255,15 @@ class Interp:
         dt = _tdt(d.dtype)
         T = d.th * d.tw
         dw, g = self.wgrad_sum(d.g, d.g_ld, d.x, d.x_ld, d.n, d.oh, d.ow, d.cout, d.ih, d.iw, d.c, d.sy, d.sx, d.th,
-                               d.tw, d.dy0, d.dx0, d.ddy, d.ddx, dt)
+                               d.tw, d.dy0, d.dx0, d.ddy, d.ddx, dt, xw=d.ow if d.ws_taps else None)
         slabs = self.lib.dvie_wgrad_slabs(ctypes.byref(d))
-        out = [("dW slabs", d.ws, (slabs, d.cout, T * d.c), (d.cout * T * d.c, T * d.c, 1), torch.float32,
-                dw.reshape(d.cout, T * d.c), "slab")]
+        if d.ws_taps:  # a phase launch of a shared slab set: its taps' column blocks only
+            K = d.ws_taps * d.c
+            out = [(f"dW slabs tap {t} -> {(d.tmap >> 4 * t) & 15}", d.ws + 4 * ((d.tmap >> 4 * t) & 15) * d.c,
+                    (slabs, d.cout, d.c), (d.cout * K, K, 1), torch.float32, dw[:, t], "slab") for t in range(T)]
+        else:
+            out = [("dW slabs", d.ws, (slabs, d.cout, T * d.c), (d.cout * T * d.c, T * d.c, 1), torch.float32,
+                    dw.reshape(d.cout, T * d.c), "slab")]
         if d.bws:
             bs = self.lib.dvie_wgrad_bias_slabs(ctypes.byref(d))
             out.append(("db slabs", d.bws, (bs, d.cout), (d.cout, 1), torch.float32, g.sum((0, 1, 2)), "slab"))

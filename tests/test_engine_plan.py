@@ -70,7 +70,13 @@ def test_hrnet_plan_structure(dtype, fused, monkeypatch):
     assert kinds[L.OP_WGRAD] == n_ref - n_head3 - 3 * n_seg
     n_s2 = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2)
     n_dgrad = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.x.buf.needs_grad)
-    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * n_s2 - n_head3 - 2 * n_seg
+    # bf16: the stride-2 data gradients with <= 128 input channels run as ONE phase-split
+    # launch (dvie_conv_desc.phc) instead of four
+    n_ph4 = sum(1 for o in plan.bwd if o.kind == L.OP_CONV and o.u.conv.phc)
+    n_ph4_want = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2 and op.x.buf.needs_grad
+                     and op.layer.cin_p <= 128) if dtype == torch.bfloat16 else 0
+    assert n_ph4 == n_ph4_want
+    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * (n_s2 - n_ph4) - n_head3 - 2 * n_seg
     # every buffer that needs a gradient received all of its contributions
     for b in g.buffers:
         if b.needs_grad and b.expected:

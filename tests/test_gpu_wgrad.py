@@ -81,3 +81,78 @@ def test_wgrad_with_bias_partials(dev, case):
     print(f"{case}: weight rel L2 {ew:.2e}, bias rel L2 {eb:.2e} ({bslabs} bias slabs)")
     assert torch.isfinite(dw).all() and torch.isfinite(db).all()
     assert ew <= 1e-4 and eb <= 1e-4, (ew, eb)
+
+
+S2_CASES = [  # n, H, W (input; even, W/2 % 64 == 0), c, x_ld, cout
+    (2, 34, 256, 64, 64, 128),      # fuse_layers.1.0 shape class, ragged row tiles
+    (1, 64, 128, 256, 256, 128),    # transition1.1 (256 -> 128)
+    (2, 40, 256, 128, 136, 256),    # 128 -> 256 from a channel slice of a wider buffer
+    (1, 18, 128, 64, 64, 64),       # fuse_layers.2.0.0 (64 -> 64)
+    (8, 128, 256, 128, 128, 256),   # transition2.2 at the bench shape
+]
+
+
+@pytest.mark.parametrize("n,H,W,c,x_ld,cout", S2_CASES)
+def test_wgrad_stride2_phase_launches(dev, n, H, W, c, x_ld, cout):
+    """The stride-2 3x3 weight gradient as the engine lowers it (engine._emit_wgrad_s2): four
+    stride-1 halo launches over the phase views x[2r + a][2q + b] (x + (a W + b) x_ld,
+    x_ld' = 2 x_ld, ih = H / 2, iw = W as the row pitch), each writing its taps' column blocks
+    (tmap) of ONE [splits][cout][9 c] slab set (ws_taps = 9), the bias partials on the (0, 0)
+    launch, then one dvie_wgrad_reduce each -- against torch's conv2d weight gradient
+    (stride 2, padding 1) and the output-gradient column sums.  The slab set starts as NaN,
+    so a tap column no launch writes shows."""
+    lib = L.load()
+    torch.manual_seed(11 + c + cout)
+    oh, ow = H // 2, W // 2
+    x = torch.randn(n, H, W, x_ld, device=dev).to(torch.bfloat16)
+    g = torch.randn(n, oh, ow, cout, device=dev).to(torch.bfloat16)
+    s = L.stream_ptr(dev)
+    descs, slabs, bslabs = [], None, 0
+    for a in (0, 1):
+        for b in (0, 1):
+            d = L.WgradDesc()
+            d.g, d.x = g.data_ptr(), x.data_ptr() + (a * W + b) * x_ld * 2
+            d.g_ld, d.x_ld = cout, 2 * x_ld
+            d.n, d.oh, d.ow, d.cout = n, oh, ow, cout
+            d.ih, d.iw, d.c, d.sy, d.sx = H // 2, W, c, 1, 1
+            d.th, d.tw, d.dy0, d.dx0, d.ddy, d.ddx = 1 + a, 1 + b, -a, -b, 1, 1
+            khs, kws = ([1] if a == 0 else [0, 2]), ([1] if b == 0 else [0, 2])
+            d.tmap = sum((kh * 3 + kw) << (4 * (i * len(kws) + j)) for i, kh in enumerate(khs) for j, kw in enumerate(kws))
+            d.ws_taps, d.dtype = 9, L.BF16
+            d.splits = lib.dvie_wgrad_splits_hint(ctypes.byref(d))
+            assert d.splits > 0
+            ns = lib.dvie_wgrad_slabs(ctypes.byref(d))
+            assert slabs in (None, ns)
+            slabs = ns
+            if a == 0 and b == 0:
+                d.bws = 1
+                bslabs = lib.dvie_wgrad_bias_slabs(ctypes.byref(d))
+            descs.append(d)
+    wfl = slabs * cout * 9 * c
+    ws = torch.full((wfl + bslabs * cout,), float("nan"), device=dev)
+    lib.dvie_trace_kernels(1)
+    for d in descs:
+        d.ws = ws.data_ptr()
+        if d.bws:
+            d.bws = ws.data_ptr() + 4 * wfl
+        L.check(lib.dvie_conv2d_wgrad(ctypes.byref(d), s), "wgrad s2 phase")
+    dw = torch.empty(cout, c, 3, 3, device=dev)
+    db = torch.empty(cout, device=dev)
+    for out, nsl, k_, ws_k, off, cin in ((dw, slabs, 3, 9 * c, 0, c), (db, bslabs, 1, 1, wfl, 1)):
+        r = L.WreduceDesc()
+        r.ws, r.dw, r.cmap = ws.data_ptr() + 4 * off, out.data_ptr(), None
+        r.splits, r.ws_rows, r.ws_k, r.co_off = nsl, cout, ws_k, 0
+        r.cout_p, r.cin_p, r.kh_n, r.kw_n, r.c, r.beta = cout, cin, k_, k_, cin if k_ > 1 else 1, 0
+        L.check(lib.dvie_wgrad_reduce(ctypes.byref(r), s), "wreduce")
+    torch.cuda.synchronize()
+    names = lib.dvie_traced_kernels().decode()
+    lib.dvie_trace_kernels(0)
+    assert names.count("wgrad_halo_kernel") == 4 and "wgrad_kernel<" not in names, names
+    xr, gr = x[..., :c].float().permute(0, 3, 1, 2).cpu(), g.float().permute(0, 3, 1, 2).cpu()
+    ref_w = torch.nn.grad.conv2d_weight(xr, (cout, c, 3, 3), gr, stride=2, padding=1)
+    ref_b = gr.sum((0, 2, 3))
+    ew = float((dw.cpu() - ref_w).norm() / ref_w.norm())
+    eb = float((db.cpu() - ref_b).norm() / ref_b.norm())
+    print(f"s2 phase wgrad n{n} {H}x{W} {c}->{cout}: weight rel L2 {ew:.2e}, bias {eb:.2e}, {slabs} slabs")
+    assert torch.isfinite(dw).all() and torch.isfinite(db).all()
+    assert ew <= 1e-4 and eb <= 1e-4, (ew, eb)

@@ -214,3 +214,33 @@ def test_bf16_fused_backward_descriptors_per_tensor(monkeypatch):
     e = rel_l2(got, ref)
     print(f"  rgb_layer.2 dh (bf16)     rel L2 {e:.2e}")
     assert e <= 4e-3
+
+
+def test_stride2_one_launch_lowerings_equal_the_per_phase_forms(monkeypatch):
+    """The stride-2 lowerings of the bf16 plan -- the data gradient as ONE phase-split launch
+    (dvie_conv_desc.phc) and the weight gradient as four phase-view launches into one shared
+    9-tap slab set (dvie_wgrad_desc.ws_taps / tmap) -- give the same parameter and input
+    gradients as the per-phase / per-tap forms they replace (DVIE_PH4=0, DVIE_WGRAD_S2=0),
+    with the interpreter as executor.  32 x 256 so that every stride-2 layer's output width
+    is a multiple of 64 (the phase-view condition) and both lowerings are taken (DVIE_WGRAD_S2=2:
+    every eligible layer, not only the >= 256-channel inputs of the default)."""
+    from deep_video_interpolation_extrapolation_amd import _lib as L
+    res = {}
+    for tag, env in (("new", {"DVIE_WGRAD_S2": "2"}), ("old", {"DVIE_PH4": "0", "DVIE_WGRAD_S2": "0"})):
+        with monkeypatch.context() as mp:
+            for k, v in env.items():
+                mp.setenv(k, v)
+            m, x, seg, w1, w2, rgb, s, ex = _run(mp, "bf16", H=32, W=256)
+            plan = m.coarse_model.last_plan
+            n_ph = sum(1 for o in plan.bwd if o.kind == L.OP_CONV and o.u.conv.phc)
+            n_ws = sum(1 for o in plan.bwd if o.kind == L.OP_WGRAD and o.u.wgrad.ws_taps)
+            res[tag] = ({k: p.grad.clone() for k, p in m.coarse_model.named_parameters()}, n_ph, n_ws)
+    g_new, n_ph, n_ws = res["new"]
+    g_old, n_ph0, n_ws0 = res["old"]
+    print(f"one-launch stride-2 data gradients {n_ph}, phase-view weight-gradient launches {n_ws}")
+    assert n_ph0 == 0 and n_ws0 == 0
+    assert n_ph == 6 and n_ws == 4 * 7, (n_ph, n_ws)  # transition1.1 (256 channels) keeps four phase launches
+    errs = {k: rel_l2(g_new[k], g_old[k]) for k in g_old}
+    worst = max(errs, key=errs.get)
+    print(f"worst {errs[worst]:.2e} ({worst})")
+    assert errs[worst] <= 1e-6, (worst, errs[worst])
