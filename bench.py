@@ -156,25 +156,44 @@ def warp_roofline(dev, n, H, W, reps=20):
     s = L.stream_ptr(dev)
 
     def fwd():
-        L.check(lib.dvie_warp_fwd(ctypes.byref(d), s), "warp fwd")
+        L.check(lib.dvie_warp_fwd(ctypes.byref(d), L.stream_ptr(dev)), "warp fwd")
 
     def bwd():
-        L.check(lib.dvie_warp_bwd(ctypes.byref(d), s), "warp bwd")
+        L.check(lib.dvie_warp_bwd(ctypes.byref(d), L.stream_ptr(dev)), "warp bwd")
 
+    # The launches are timed two ways: replayed from a captured hipGraph of `reps` launches
+    # (the GPU time per launch: at 256x512 a launch is ~7 us, about what the Python ctypes
+    # call + hipLaunchKernel take, so eager back-to-back launches leave the GPU idle between
+    # kernels), which gives `*_ms` / `*_frac`; and eagerly from Python (`*_ms_eager`).
     res = {}
     for tag, fn, bpp in (("fwd", fwd, 32.0), ("bwd", bwd, 52.0)):
         for _ in range(3):
             fn()
+        torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
             fn()
         e1.record()
         torch.cuda.synchronize()
+        ms_eager = e0.elapsed_time(e1) / reps
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
+        del g
         gbs = bpp * n * H * W / (ms * 1e-3) / 1e9
         res[tag + "_ms"], res[tag + "_GBps"], res[tag + "_frac"] = round(ms, 4), round(gbs, 1), round(gbs / PEAK_HBM_GBS, 4)
-    res.update(shape=[n, 3, H, W], bytes_per_px={"fwd": 32, "bwd": 52},
+        res[tag + "_ms_eager"] = round(ms_eager, 4)
+        res[tag + "_frac_eager"] = round(bpp * n * H * W / (ms_eager * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+    res.update(shape=[n, 3, H, W], bytes_per_px={"fwd": 32, "bwd": 52}, timing="hipGraph replay of back-to-back launches",
                flow="smooth, |dx| <= %.1f px, |dy| <= %.1f px" % (0.016 * (W - 1) / 2, 0.024 * (H - 1) / 2))
     return res
 

@@ -90,7 +90,10 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 // AB: timing-only ablations, compiled into -DDVIE_TIMING_DBG builds only (DVIE_WG_DBG): 8 = no
 // DMA after the first tile (stale operands), 16 = no MFMAs, 32 = no slab stores, 64 = no LDS
 // fragment reads after a tile's first two k-steps, 128 = no end-of-tile wait and barrier
-template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8, bool PIPE = false, int AB = 0>
+// DOB (PIPE form): the bias column sums are compiled in (a launch with p.bws); without them
+// the k-steps carry no v_dot2c (most HRNet convs have no bias: 4 of them per k-step per wave
+// sat beside the MFMAs for nothing)
+template <int TH, int TW, int PR, int TMO, int TMI, int NW = 8, bool PIPE = false, int AB = 0, bool DOB = true>
 __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_desc p, int n_co, int n_ci, int splits,
                                                              int tiles_x, int tiles_y, int n_tiles, int flags) {
   typedef WgCfg<TH, TW, PR, TMO, TMI> C;
@@ -266,7 +269,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
   const int wco = NW == 8 ? (wave >> 1) & 1 : 0, wci = wave & 1, wrow = NW == 8 ? wave >> 2 : wave >> 1;
   // bias gradient (p.bws): the ci-block-0 workgroups' wci = 0 waves sum the G fragments they
   // already hold for the MFMAs (lane l: co = l % 32 of the fragment, 8 pixels)
-  const bool dob = p.bws != nullptr && kb == 0 && wci == 0;
+  const bool dob = DOB && p.bws != nullptr && kb == 0 && wci == 0;
   float bsum[TMO];
 #pragma unroll
   for (int j = 0; j < TMO; ++j) bsum[j] = 0.f;
@@ -307,7 +310,18 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
     const char* X = smem + 2 * C::GSZ;
     if constexpr (PIPE) {
       constexpr int NS = (PR / 2) * 4, NB = C::NT * TMI;
-      const int ys = T.y0 % C::R;  // ring slot of the tile's first halo row
+      // LDS bases of the halo rows this wave's k-steps read (rows wrow * PR/2 + j of the tile),
+      // ring wrap resolved once per tile rather than per k-step and tap
+      constexpr int NXR = PR / 2 + TH - 1;
+      const char* Xrow[NXR];
+      {
+        int slot = (T.y0 + wrow * (PR / 2)) % C::R;
+#pragma unroll
+        for (int j = 0; j < NXR; ++j) {
+          Xrow[j] = X + slot * (C::XW * 128);
+          slot = slot + 1 == C::R ? 0 : slot + 1;
+        }
+      }
       bf16x8 pa[2][TMO], pb[2][NB];
       auto load = [&](int st, int k) {
         if ((dbg & 64) && st >= 2) return;
@@ -317,9 +331,7 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
         for (int j = 0; j < TMO; ++j) pa[k][j] = tr_pair(G + g_off[j] + gr * 128, G + g_off[j] + gr * 128 + 4 * 128);
 #pragma unroll
         for (int ti = 0; ti < TH; ++ti) {
-          int slot = ys + py + ti;  // < 2R
-          slot -= slot >= C::R ? C::R : 0;
-          const char* Xr = X + slot * (C::XW * 128);
+          const char* Xr = Xrow[(st >> 2) + ti];
 #pragma unroll
           for (int tj = 0; tj < TW; ++tj) {
             const int xr = kx * 16 + tj;
@@ -345,8 +357,10 @@ __global__ __launch_bounds__(64 * NW) void wgrad_halo_kernel(const dvie_wgrad_de
               else
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[k][jo], b, c, 0, 0, 0);
             }
+        if constexpr (DOB) {
 #pragma unroll
-        for (int j = 0; j < TMO; ++j) bsum[j] = sum8_bf16(pa[k][j], bsum[j]);
+          for (int j = 0; j < TMO; ++j) bsum[j] = sum8_bf16(pa[k][j], bsum[j]);
+        }
       };
       load(0, 0);
 #pragma unroll
@@ -754,15 +768,24 @@ bool wgrad_halo_launch(const dvie_wgrad_desc& p, hipStream_t s) {
     }
   }
 #endif
-  if (p.th == 3 && p.cout > 32 && wg_pipe)
+  if (p.th == 3 && p.cout > 32 && wg_pipe && !p.bws)
+    DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true, 0, false>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci,
+                p.splits, tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
+  else if (p.th == 3 && p.cout > 32 && wg_pipe)
     DVIE_LAUNCH((wgrad_halo_kernel<3, 3, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
                        tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   // the stride-2 weight gradient's phase launches (ws_taps): 2 x 2, 2 x 1, 1 x 2 tap grids
 #define DVIE_WG2(TH, TW)                                                                                        \
+  else if (p.th == TH && p.tw == TW && !p.bws)                                                                  \
+    DVIE_LAUNCH((wgrad_halo_kernel<TH, TW, 4, 1, 1, 8, true, 0, false>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, \
+                p.splits, tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);                                        \
   else if (p.th == TH && p.tw == TW)                                                                            \
     DVIE_LAUNCH((wgrad_halo_kernel<TH, TW, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits, \
                 tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   DVIE_WG2(2, 2) DVIE_WG2(2, 1) DVIE_WG2(1, 2)
+  else if (p.ws_taps > 0 && p.th == 1 && p.tw == 1 && !p.bws)
+    DVIE_LAUNCH((wgrad_halo_kernel<1, 1, 4, 1, 1, 8, true, 0, false>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci,
+                p.splits, tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
   else if (p.ws_taps > 0 && p.th == 1 && p.tw == 1)
     DVIE_LAUNCH((wgrad_halo_kernel<1, 1, 4, 1, 1, 8, true>), dim3(grid), dim3(512), 0, s, p, n_co, n_ci, p.splits,
                 tiles_x, tiles_y, n_tiles, wg_merge | wg_setprio);
