@@ -165,8 +165,12 @@ def warp_roofline(dev, n, H, W, reps=20):
     # (the GPU time per launch: at 256x512 a launch is ~7 us, about what the Python ctypes
     # call + hipLaunchKernel take, so eager back-to-back launches leave the GPU idle between
     # kernels), which gives `*_ms` / `*_frac`; and eagerly from Python (`*_ms_eager`).
+    def floor():  # an empty kernel on the forward's grid (dvie_warp_fwd: 4 waves per block)
+        waves = n * H * ((W + 255) // 256)
+        L.check(lib.dvie_launch_probe(min((waves + 3) // 4, 8192), 256, L.stream_ptr(dev)), "launch probe")
+
     res = {}
-    for tag, fn, bpp in (("fwd", fwd, 32.0), ("bwd", bwd, 52.0)):
+    for tag, fn, bpp in (("fwd", fwd, 32.0), ("bwd", bwd, 52.0), ("floor", floor, 0.0)):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -189,6 +193,11 @@ def warp_roofline(dev, n, H, W, reps=20):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         del g
+        if tag == "floor":  # the forward's launch floor: an empty kernel of its grid
+            res["fwd_launch_floor_ms"] = round(ms, 4)
+            res["fwd_frac_above_floor"] = round(32.0 * n * H * W / ((res["fwd_ms"] - ms) * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) \
+                if res["fwd_ms"] > ms else None
+            continue
         gbs = bpp * n * H * W / (ms * 1e-3) / 1e9
         res[tag + "_ms"], res[tag + "_GBps"], res[tag + "_frac"] = round(ms, 4), round(gbs, 1), round(gbs / PEAK_HBM_GBS, 4)
         res[tag + "_ms_eager"] = round(ms_eager, 4)

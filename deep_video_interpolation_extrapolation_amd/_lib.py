@@ -22,6 +22,7 @@ LOSS_L1, LOSS_GDL, LOSS_SSIM, LOSS_MSE, LOSS_CE, LOSS_L1NHWC, LOSS_COSNHWC, LOSS
 OP_CONV, OP_WGRAD, OP_WREDUCE, OP_COLSUM, OP_EW, OP_LOSS, OP_PACK = 1, 2, 3, 4, 5, 6, 7
 OP_BN_FWD, OP_BN_BWD, OP_HEAD_FWD, OP_HEAD_BWD, OP_ATTN, OP_HEAD3_BWD, OP_SEGENC_FWD = 8, 9, 10, 11, 12, 13, 14
 OP_SEGENC_BWD = 15
+OP_WREDUCE_MULTI = 16
 (ATTN_L2NORM, ATTN_L2NORM_BWD, ATTN_CORR, ATTN_GATHER, ATTN_GATHER_T, ATTN_SOFTMAX, ATTN_SOFTMAX_BWD, ATTN_WNORM,
  ATTN_WNORM_BWD, ATTN_POOL, ATTN_POOL_T) = range(11)
 
@@ -207,11 +208,17 @@ class SegencBwdDesc(ctypes.Structure):
     ]
 
 
+class WreduceMultiDesc(ctypes.Structure):
+    """several dvie_wreduce_desc in one launch: `descs` is a HOST array, read at launch time"""
+    _fields_ = [("descs", vp), ("n", i32), ("pad", i32)]
+
+
 class _OpUnion(ctypes.Union):
     _fields_ = [
         ("conv", ConvDesc), ("wgrad", WgradDesc), ("wreduce", WreduceDesc), ("colsum", ColsumDesc),
         ("ew", EwDesc), ("loss", LossDesc), ("pack", PackList), ("bn", BnDesc), ("head", HeadDesc),
         ("attn", AttnDesc), ("head3", Head3BwdDesc), ("segenc", SegencDesc), ("segenc_bwd", SegencBwdDesc),
+        ("wreduce_multi", WreduceMultiDesc),
     ]
 
 
@@ -221,16 +228,16 @@ class Op(ctypes.Structure):
 
 _ABI = {0: Op, OP_CONV: ConvDesc, OP_WGRAD: WgradDesc, OP_WREDUCE: WreduceDesc, OP_COLSUM: ColsumDesc,
         OP_EW: EwDesc, OP_LOSS: LossDesc, OP_PACK: PackDesc, OP_BN_FWD: BnDesc, OP_HEAD_FWD: HeadDesc,
-        OP_ATTN: AttnDesc, OP_HEAD3_BWD: Head3BwdDesc, OP_SEGENC_FWD: SegencDesc, OP_SEGENC_BWD: SegencBwdDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
+        OP_ATTN: AttnDesc, OP_HEAD3_BWD: Head3BwdDesc, OP_SEGENC_FWD: SegencDesc, OP_SEGENC_BWD: SegencBwdDesc, OP_WREDUCE_MULTI: WreduceMultiDesc, 100: WarpDesc, 101: SoftmaxDesc, 102: SnLayer, 103: ClipDesc}
 
 EXPORTS = [
-    "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_colsum", "dvie_pack_weights",
+    "dvie_conv2d_fwd", "dvie_conv2d_wgrad", "dvie_wgrad_splits_hint", "dvie_wgrad_slabs", "dvie_wgrad_reduce", "dvie_wgrad_reduce_multi", "dvie_colsum", "dvie_pack_weights",
     "dvie_ew", "dvie_loss", "dvie_loss_partial_count", "dvie_loss_ws_floats", "dvie_warp_fwd",
     "dvie_warp_bwd", "dvie_adamax", "dvie_scale", "dvie_run_ops", "dvie_abi_sizeof", "dvie_version",
     "dvie_last_error", "dvie_bn_fwd", "dvie_bn_bwd", "dvie_bn_partial_splits", "dvie_head_fwd", "dvie_head_bwd",
     "dvie_softmax_fwd", "dvie_softmax_bwd", "dvie_adam", "dvie_sn_fwd", "dvie_sn_bwd", "dvie_reparam_fwd",
     "dvie_reparam_bwd", "dvie_warp_ws_floats", "dvie_clip_prep", "dvie_attn", "dvie_step_inc", "dvie_adamax_dev",
-    "dvie_adam_dev", "dvie_mfma_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs", "dvie_head3_bwd",
+    "dvie_adam_dev", "dvie_mfma_probe", "dvie_launch_probe", "dvie_sum_f32", "dvie_wgrad_bias_slabs", "dvie_head3_bwd",
     "dvie_segenc_fwd", "dvie_segenc_bwd", "dvie_pack_blocks", "dvie_trace_kernels", "dvie_traced_kernels",
 ]
 
@@ -270,6 +277,8 @@ def load():
             getattr(lib, name).argtypes = [vp, vp]
             getattr(lib, name).restype = i32
         lib.dvie_pack_weights.argtypes = [vp, i32, i32, vp]
+        lib.dvie_wgrad_reduce_multi.argtypes = [vp, i32, vp]
+        lib.dvie_wgrad_reduce_multi.restype = i32
         lib.dvie_trace_kernels.argtypes = [i32]
         lib.dvie_trace_kernels.restype = i32
         lib.dvie_traced_kernels.argtypes = []
@@ -293,6 +302,8 @@ def load():
         lib.dvie_step_inc.argtypes = [vp, vp]
         lib.dvie_mfma_probe.argtypes = [vp, i32, i32, vp]
         lib.dvie_mfma_probe.restype = i32
+        lib.dvie_launch_probe.argtypes = [i32, i32, vp]
+        lib.dvie_launch_probe.restype = i32
         lib.dvie_sum_f32.argtypes = [vp, i32, vp, vp]
         lib.dvie_sum_f32.restype = i32
         lib.dvie_wgrad_bias_slabs.argtypes = [vp]

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const dvie_wgrad_desc p, lon
 // scatter into the OIHW gradient.  Wide reductions (weights) use 32 x 8; narrow ones with
 // many slabs (bias column sums: cout/4 columns, thousands of partials) 4 x 64.
 template <int QB, int SL>
-__global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p) {
+__device__ __forceinline__ void wreduce_block(const dvie_wreduce_desc& p, int bx) {
   static_assert(QB * SL == 256, "block shape");
   __shared__ double red[SL][QB][4];
   const int tid = threadIdx.x;
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p)
   const int taps = p.kh_n * p.kw_n;
   const long long total4 = (long long)(p.ws_rows - p.co_off) * p.ws_k / 4;  // scanned (padded) rows
   const long long slab = (long long)p.ws_rows * p.ws_k;
-  const long long q = (long long)blockIdx.x * QB + ql;
+  const long long q = (long long)bx * QB + ql;
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   if (q < total4) {
     const float* src = p.ws + (long long)p.co_off * p.ws_k + q * 4;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p)
   __syncthreads();
   if (tid < QB * 4) {
     const int qq = tid >> 2, e = tid & 3;
-    const long long f = ((long long)blockIdx.x * QB + qq) * 4 + e;
+    const long long f = ((long long)bx * QB + qq) * 4 + e;
     if (f < total4 * 4) {
       double s = 0;
       for (int k = 0; k < SL; ++k) s += red[k][qq][e];
@@ -332,6 +332,25 @@ __global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p)
       }
     }
   }
+}
+
+template <int QB, int SL>
+__global__ __launch_bounds__(256) void wreduce_kernel(const dvie_wreduce_desc p) {
+  wreduce_block<QB, SL>(p, blockIdx.x);
+}
+
+// up to WRM reductions in one launch: descriptor i owns blocks [blk0[i], blk0[i + 1])
+constexpr int WRM = 16;
+struct WreduceMulti {
+  dvie_wreduce_desc d[WRM];
+  int blk0[WRM + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wreduce_multi_kernel(const WreduceMulti m) {
+  int i = 0;
+  while (i + 1 < m.n && (int)blockIdx.x >= m.blk0[i + 1]) ++i;  // (uniform per block)
+  wreduce_block<32, 8>(m.d[i], (int)blockIdx.x - m.blk0[i]);
 }
 
 template <typename T>
@@ -591,12 +610,11 @@ int dvie_conv2d_wgrad(const dvie_wgrad_desc* d, void* stream) {
   DVIE_RETURN_LAUNCH();
 }
 
+static int wreduce_check(const dvie_wreduce_desc* d);
+
 int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream) {
-  DVIE_CHECK_ARG(d && d->ws && d->dw, "wreduce: null pointer");
-  DVIE_CHECK_ARG(d->ws_k % 4 == 0 || d->ws_k == 1, "wreduce: ws_k=%d", d->ws_k);
-  DVIE_CHECK_ARG(((long long)d->co_off * d->ws_k) % 4 == 0 && d->ws_rows * (long long)d->ws_k % 4 == 0,
-                 "wreduce: slab alignment (ws_rows*ws_k and co_off*ws_k multiples of 4)");
-  DVIE_CHECK_ARG(d->co_off + d->cout_p <= d->ws_rows, "wreduce: rows");
+  const int rc = wreduce_check(d);
+  if (rc != DVIE_OK) return rc;
   const long long total4 = (long long)(d->ws_rows - d->co_off) * d->ws_k / 4;
   if (total4 < 1) return DVIE_OK;
   if (total4 < 2048 && d->splits >= 256)
@@ -605,6 +623,38 @@ int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream) {
   else
     DVIE_LAUNCH((wreduce_kernel<32, 8>), dim3((unsigned)((total4 + 31) / 32)), dim3(256), 0,
                        (hipStream_t)stream, *d);
+  DVIE_RETURN_LAUNCH();
+}
+
+static int wreduce_check(const dvie_wreduce_desc* d) {
+  DVIE_CHECK_ARG(d && d->ws && d->dw, "wreduce: null pointer");
+  DVIE_CHECK_ARG(d->ws_k % 4 == 0 || d->ws_k == 1, "wreduce: ws_k=%d", d->ws_k);
+  DVIE_CHECK_ARG(((long long)d->co_off * d->ws_k) % 4 == 0 && d->ws_rows * (long long)d->ws_k % 4 == 0,
+                 "wreduce: slab alignment (ws_rows*ws_k and co_off*ws_k multiples of 4)");
+  DVIE_CHECK_ARG(d->co_off + d->cout_p <= d->ws_rows, "wreduce: rows");
+  return DVIE_OK;
+}
+
+int dvie_wgrad_reduce_multi(const dvie_wreduce_desc* descs, int n, void* stream) {
+  DVIE_CHECK_ARG(descs && n >= 0, "wreduce_multi: args");
+  for (int base = 0; base < n; base += WRM) {
+    WreduceMulti m;
+    m.n = 0;
+    int blocks = 0;
+    for (int i = base; i < n && i < base + WRM; ++i) {
+      const int rc = wreduce_check(&descs[i]);
+      if (rc != DVIE_OK) return rc;
+      const long long total4 = (long long)(descs[i].ws_rows - descs[i].co_off) * descs[i].ws_k / 4;
+      if (total4 < 1) continue;
+      m.d[m.n] = descs[i];
+      m.blk0[m.n] = blocks;
+      blocks += (int)((total4 + 31) / 32);
+      ++m.n;
+    }
+    m.blk0[m.n] = blocks;
+    if (m.n == 0) continue;
+    DVIE_LAUNCH(wreduce_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, m);
+  }
   DVIE_RETURN_LAUNCH();
 }
 

@@ -60,6 +60,8 @@ __global__ __launch_bounds__(256) void mfma_probe_kernel(float* out, int iters) 
   out[g] = s;
 }
 
+__global__ void launch_probe_kernel() {}
+
 }  // namespace dvie
 
 using namespace dvie;
@@ -67,5 +69,11 @@ using namespace dvie;
 extern "C" int dvie_mfma_probe(float* out, int blocks, int iters, void* stream) {
   DVIE_CHECK_ARG(out && blocks > 0 && iters > 0, "mfma_probe: args");
   DVIE_LAUNCH(mfma_probe_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, iters);
+  DVIE_RETURN_LAUNCH();
+}
+
+extern "C" int dvie_launch_probe(int blocks, int threads, void* stream) {
+  DVIE_CHECK_ARG(blocks > 0 && threads > 0 && threads <= 1024, "launch_probe: args");
+  DVIE_LAUNCH(launch_probe_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream);
   DVIE_RETURN_LAUNCH();
 }

@@ -749,10 +749,17 @@ int dvie_run_ops(const dvie_op* ops, int n, void* stream) {
       lr.tail_fresh = false;  // the caller's stream moves on past the weight lane's wait
     }
     void* s = (void*)st;
+#ifdef DVIE_TIMING_DBG
+    // timing-only ablation (-DDVIE_TIMING_DBG builds, wrong results): DVIE_SKIP_KINDS = bit mask
+    // of op kinds left out, e.g. the weight-gradient reductions, to price them in the step
+    static const long long skip_kinds = getenv("DVIE_SKIP_KINDS") ? atoll(getenv("DVIE_SKIP_KINDS")) : 0;
+    if ((skip_kinds >> o.kind) & 1) continue;
+#endif
     switch (o.kind) {
       case DVIE_OP_CONV: rc = dvie_conv2d_fwd(&o.u.conv, s); break;
       case DVIE_OP_WGRAD: rc = dvie_conv2d_wgrad(&o.u.wgrad, s); break;
       case DVIE_OP_WREDUCE: rc = dvie_wgrad_reduce(&o.u.wreduce, s); break;
+      case DVIE_OP_WREDUCE_MULTI: rc = dvie_wgrad_reduce_multi(o.u.wreduce_multi.descs, o.u.wreduce_multi.n, s); break;
       case DVIE_OP_COLSUM: rc = dvie_colsum(&o.u.colsum, s); break;
       case DVIE_OP_EW: rc = dvie_ew(&o.u.ew, s); break;
       case DVIE_OP_LOSS: rc = dvie_loss(&o.u.loss, s); break;
@@ -786,6 +793,7 @@ size_t dvie_abi_sizeof(int which) {
     case DVIE_OP_CONV: return sizeof(dvie_conv_desc);
     case DVIE_OP_WGRAD: return sizeof(dvie_wgrad_desc);
     case DVIE_OP_WREDUCE: return sizeof(dvie_wreduce_desc);
+    case DVIE_OP_WREDUCE_MULTI: return sizeof(dvie_wreduce_multi_desc);
     case DVIE_OP_COLSUM: return sizeof(dvie_colsum_desc);
     case DVIE_OP_EW: return sizeof(dvie_ew_desc);
     case DVIE_OP_LOSS: return sizeof(dvie_loss_desc);

@@ -701,8 +701,8 @@ int wgrad_halo_splits(const dvie_wgrad_desc& p) {
   int tx, ty, nt, nco, nci;
   wgrad_tiles(p, w, tx, ty, nt, nco, nci);
   int s = 256 / (nco * nci);  // one workgroup per CU (LDS-bound): a single wave of workgroups
-  const char* e = getenv("DVIE_WG_SPLITS");  // tuning: multiplier of that split count
-  if (e && *e && atoi(e) > 0) s *= atoi(e);
+  const char* e = getenv("DVIE_WG_SPLITS");  // tuning: multiplier of that split count (e.g. 0.5)
+  if (e && *e && atof(e) > 0) s = (int)(s * atof(e) + 0.5);
   if (s > nt) s = nt;
   return s < 1 ? 1 : s;
 }

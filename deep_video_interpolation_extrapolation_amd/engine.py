@@ -1787,27 +1787,148 @@ class Plan:
             self._contrib(x, em)
 
     # ---------------- finalize ----------------
+    def _batch_reductions(self):
+        """The weight lane's slab reductions in batches of up to 16, each batch ONE
+        dvie_wgrad_reduce_multi launch where its last reduction was (include/dvie.h).  Without
+        batching every slab writer (weight gradient / column sums) shares offset 0 of self.ws,
+        each reduced right after it is written; in a batch each writer gets its own region
+        (consecutive writers with no reduction between them -- the stride-2 phase launches of
+        one slab set -- share one), so the reductions can wait for the batch's end.  Measured
+        with the timing-only skip (tools/skip_ab.sh): the 73 one-by-one reductions cost the eager
+        step 0.8 ms of its 31.3.  DVIE_WREDUCE_MULTI=0 keeps them one by one."""
+        if os.environ.get("DVIE_WREDUCE_MULTI", "1") == "0" or not self.bwd:
+            return
+        MAXN = 16
+        budget = int(float(os.environ.get("DVIE_WREDUCE_MB", "1024")) * 2 ** 20 / 4)  # floats per batch
+        # pass 1: reductions reading self.ws -> their writer; region sizes per writer group
+        writer_of, size, cur, had_reduce = {}, {}, None, True
+        for i, o in enumerate(self.bwd):
+            if o.kind in (L.OP_WGRAD, L.OP_COLSUM):
+                if had_reduce or cur is None:
+                    cur, had_reduce = i, False
+                writer_of[i] = cur
+            elif o.kind == L.OP_WREDUCE:
+                had_reduce = True
+                if getattr(o, "ws_ptr", None) is None:
+                    r = o.u.wreduce
+                    writer_of[i] = cur
+                    size[cur] = max(size.get(cur, 0), getattr(o, "ws_off", 0) + r.splits * r.ws_rows * r.ws_k)
+        # pass 2: batches, regions, the multi ops
+        new, remap, pending, base, off, live_end = [], {}, [], {}, 0, 0
+        self._multi = []  # (host descriptor array, [(ws_ptr or None, float offset in self.ws)])
+
+        def flush():
+            nonlocal pending, off
+            if not pending:
+                return
+            arr = (L.WreduceDesc * len(pending))()
+            wsrc = []
+            for j, (oi, o) in enumerate(pending):
+                arr[j] = o.u.wreduce
+                wp = getattr(o, "ws_ptr", None)
+                wsrc.append((wp, None if wp else base[writer_of[oi]] + getattr(o, "ws_off", 0)))
+            m = self._op(L.OP_WREDUCE_MULTI)
+            m.u.wreduce_multi.descs = ctypes.addressof(arr)
+            m.u.wreduce_multi.n = len(pending)
+            metas = [getattr(o, "meta", None) or {} for _, o in pending]
+            m.meta = dict(cls="wgrad_reduce", name=f"{len(pending)} reductions ({metas[0].get('name', '')} ..)",
+                          flops=0.0, bytes=float(sum(mt.get("bytes", 0.0) for mt in metas)))
+            self._multi.append((arr, wsrc))
+            for oi, _ in pending:
+                remap[oi] = len(new)
+            new.append(m)
+            pending, off = [], 0
+
+        # a batch's reductions run concurrently: two that accumulate into one gradient (a layer
+        # used twice, e.g. the seg encoder on both segmentation maps) go to different batches
+        target = {idx: (id(lay), which) for idx, lay, which, _ in self._grad_slots if which != "bn"}
+        for i, o in enumerate(self.bwd):
+            if o.kind == L.OP_WREDUCE and i in target and any(target.get(oi) == target[i] for oi, _ in pending):
+                flush()
+                off = live_end  # the latest region may still be read: the next ones go after it
+            if o.kind in (L.OP_WGRAD, L.OP_COLSUM):
+                w = writer_of[i]
+                if w == i:  # a new slab region
+                    need = size.get(w, 0)
+                    if pending and off + need > budget:
+                        flush()  # (every earlier region has all its reductions in that batch)
+                    base[w] = off
+                    off += need
+                    live_end = off
+                self.ws_floats = max(self.ws_floats, base[w] + size.get(w, 0))
+                o.ws_base = base[w]
+                remap[i] = len(new)
+                new.append(o)
+            elif o.kind == L.OP_WREDUCE:
+                pending.append((i, o))
+                if len(pending) == MAXN:
+                    flush()
+                    off = live_end  # (the latest region's other reductions may follow)
+            else:
+                remap[i] = len(new)
+                new.append(o)
+        flush()
+        self.bwd = new
+        self.completions = [(remap[idx - 1] + 1, lay) for idx, lay in self.completions]
+        # backward indices recorded while building: moved with their ops
+        self.ext_ograd = {k: remap[i] for k, i in self.ext_ograd.items()}
+        if hasattr(self, "ext_head_grad"):
+            self.ext_head_grad = {k: remap[i] for k, i in self.ext_head_grad.items()}
+        self.ext_grad = {k: [(remap[i], op) for i, op in v] for k, v in self.ext_grad.items()}
+        if hasattr(self, "ext_mask"):
+            self.ext_mask = {k: [(w, remap[i] if w == "bwd" else i, op) for w, i, op in v]
+                             for k, v in self.ext_mask.items()}
+        slots = []
+        pos = {}  # multi op index -> the old indices of its reductions, in order
+        for oi, ni in sorted(remap.items()):
+            if new[ni].kind == L.OP_WREDUCE_MULTI:
+                pos.setdefault(ni, []).append(oi)
+        for idx, lay, which, first in self._grad_slots:
+            if which != "bn" and self.bwd[remap[idx]].kind == L.OP_WREDUCE_MULTI:
+                ni = remap[idx]
+                slots.append((("multi", ni, pos[ni].index(idx)), lay, which, first))
+            else:
+                slots.append((remap[idx], lay, which, first))
+        self._grad_slots = slots
+        self.n_bwd = len(self.bwd)
+
+    def _wreduce_desc(self, idx):
+        """the dvie_wreduce_desc of a gradient slot (one reduction op, or an element of a
+        batch's host array)"""
+        if isinstance(idx, tuple):
+            _, ni, j = idx
+            arr = (L.WreduceDesc * self.bwd_arr[ni].u.wreduce_multi.n).from_address(
+                self.bwd_arr[ni].u.wreduce_multi.descs)
+            return arr[j]
+        return self.bwd_arr[idx].u.wreduce
+
     def _finalize(self):
         L.load()
+        self._batch_reductions()
         # workspace for wgrad / colsum partials
         self.ws = torch.empty(max(1, self.ws_floats), dtype=torch.float32, device=self.device)
         self.keep.append(self.ws)
         wlane = _wgrad_lane()
+        wsp = self.ws.data_ptr()
         for o in self.bwd:
             # weight / bias gradients are off the data-gradient chain: they run on the
             # executor's side stream (dvie_op.lane 1), forked where their output gradient is
             # final and joined at the end of each dvie_run_ops call.  They are the only users
             # of self.ws, and they stay in order on that one stream.
-            if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM) and wlane:
+            if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM, L.OP_WREDUCE_MULTI) and wlane:
                 o.lane = 1
             if o.kind == L.OP_WGRAD:
-                o.u.wgrad.ws = self.ws.data_ptr()
+                o.u.wgrad.ws = wsp + 4 * getattr(o, "ws_base", 0)
                 if hasattr(o, "bws_off"):  # bias partials after the weight slabs
-                    o.u.wgrad.bws = self.ws.data_ptr() + 4 * o.bws_off
+                    o.u.wgrad.bws = wsp + 4 * (getattr(o, "ws_base", 0) + o.bws_off)
             elif o.kind == L.OP_COLSUM:
-                o.u.colsum.ws = self.ws.data_ptr()
+                o.u.colsum.ws = wsp + 4 * getattr(o, "ws_base", 0)
             elif o.kind == L.OP_WREDUCE:
-                o.u.wreduce.ws = getattr(o, "ws_ptr", None) or self.ws.data_ptr() + 4 * getattr(o, "ws_off", 0)
+                o.u.wreduce.ws = getattr(o, "ws_ptr", None) or wsp + 4 * getattr(o, "ws_off", 0)
+        for arr, wsrc in getattr(self, "_multi", []):
+            for j, (wp, off) in enumerate(wsrc):
+                arr[j].ws = wp if wp else wsp + 4 * off
+            self.keep.append(arr)
         # pack op (all layers, one launch) goes first in the forward list
         descs = self._pack_descs
         if not descs:  # no convolutions (e.g. a pointwise-only plan)
@@ -1957,7 +2078,7 @@ class Plan:
                     setattr(d, field, p.grad.data_ptr())
                 d.accumulate = int(accumulate) if first else 1
                 continue
-            d = self.bwd_arr[idx].u.wreduce
+            d = self._wreduce_desc(idx)
             if isinstance(lay.m, StackedConv):
                 d.dw = lay.m.grad_ptr(which)
             else:

@@ -165,6 +165,19 @@ typedef struct dvie_wreduce_desc {
 
 int dvie_wgrad_reduce(const dvie_wreduce_desc* d, void* stream);
 
+/*
+ * Several slab reductions in ONE launch (replaces as many dvie_wgrad_reduce launches; the
+ * engine batches the weight lane's reductions, each weight gradient of a batch writing its
+ * own slab region).  descs: a HOST array of n descriptors, read at launch time, so the caller
+ * may re-point their dw / beta between launches.  A flat grid: each descriptor owns a
+ * contiguous block range.  Same results as n dvie_wgrad_reduce calls.
+ */
+int dvie_wgrad_reduce_multi(const dvie_wreduce_desc* descs, int n, void* stream);
+typedef struct dvie_wreduce_multi_desc {
+  const dvie_wreduce_desc* descs; /* host array */
+  int n, pad;
+} dvie_wreduce_multi_desc;
+
 /* Bias gradient partials: part[s][co] = sum_{pix in split s} g[pix][co]. */
 typedef struct dvie_colsum_desc {
   const void* g;
@@ -391,6 +404,13 @@ int dvie_scale(float* p, long long n, float s, void* stream);
  * MFMA ceiling at the clock the chip holds under that load on this box.
  */
 int dvie_mfma_probe(float* out, int blocks, int iters, void* stream);
+
+/*
+ * Measurement only (bench.py): `blocks` workgroups of `threads` threads of an empty kernel --
+ * the dispatch / ramp / drain floor of a launch of that shape (the warp forward's grid at
+ * 256x512 is a ~7 us launch, where this floor is a large part).
+ */
+int dvie_launch_probe(int blocks, int threads, void* stream);
 
 /*
  * BatchNorm2d over NHWC rows (rows = N*H*W pixels, c channels), fused with the following
@@ -690,6 +710,7 @@ int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream);
 #define DVIE_OP_HEAD3_BWD 13
 #define DVIE_OP_SEGENC_FWD 14
 #define DVIE_OP_SEGENC_BWD 15
+#define DVIE_OP_WREDUCE_MULTI 16
 
 typedef struct dvie_pack_list {
   const dvie_pack_desc* descs_dev;
@@ -713,6 +734,7 @@ typedef struct dvie_op {
     dvie_head3_bwd_desc head3;
     dvie_segenc_desc segenc;
     dvie_segenc_bwd_desc segenc_bwd;
+    dvie_wreduce_multi_desc wreduce_multi;
   } u;
 } dvie_op;
 

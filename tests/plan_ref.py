@@ -484,6 +484,10 @@ class Interp:
             return self.ref_wgrad(o.u.wgrad)
         if k == L.OP_WREDUCE:
             return self.ref_wreduce(o.u.wreduce)
+        if k == L.OP_WREDUCE_MULTI:  # a batch of reductions: each one's result
+            m = o.u.wreduce_multi
+            descs = (L.WreduceDesc * m.n).from_address(m.descs)
+            return [out for d in descs for out in self.ref_wreduce(d)]
         if k == L.OP_COLSUM:
             return self.ref_colsum(o.u.colsum)
         if k == L.OP_EW:

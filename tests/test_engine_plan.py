@@ -142,13 +142,17 @@ def test_buckets_with_unstacked_heads(bucket_mb, monkeypatch):
     assert len(cuts) == len(ranges) - 1
     # at each cut every parameter below the range end has completed
     span = {id(p): (off, off + n) for p, (off, n, _) in zip(hr._flat_params, hr._flat_specs)}
+    # (several layers complete at one index when their reductions share a batched launch:
+    # a cut is checked once every completion at its index is counted)
     done = []
     k = 0
-    for idx, lay in plan.completions:
+    comps = plan.completions
+    for j, (idx, lay) in enumerate(comps):
         ps = lay.m.params() if isinstance(lay.m, E.StackedConv) else [lay.m.weight] + (
             [lay.m.bias] if lay.m.bias is not None else [])
         done += [span[id(p)] for p in ps]
-        if k < len(cuts) and idx == cuts[k]:
+        last_at_idx = j + 1 == len(comps) or comps[j + 1][0] != idx
+        while last_at_idx and k < len(cuts) and idx == cuts[k]:
             hi = ranges[k][1]
             assert sum(e - s for s, e in done if e <= hi) == hi
             k += 1
@@ -171,13 +175,47 @@ def test_weight_lane_tags(dtype, monkeypatch):
         n_w = 0
         for i in range(plan.n_bwd):
             o = plan.bwd_arr[i]
-            if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM):
+            if o.kind in (L.OP_WGRAD, L.OP_WREDUCE, L.OP_COLSUM, L.OP_WREDUCE_MULTI):
                 assert o.lane == wl
                 n_w += 1
             else:
                 assert o.lane == 0, o.kind
-        assert n_w > 50
+        assert n_w > 40
         assert all(plan.fwd_arr[i].lane == 0 for i in range(len(plan.fwd_arr)))
+
+
+def test_batched_reductions(monkeypatch):
+    """The weight lane's slab reductions run in batches (engine Plan._batch_reductions): no
+    one-by-one reduction left, at most 16 per batch, every parameter's gradient slot points
+    into a batch, the completion points stay ordered and after their batch, and the slab
+    regions of one batch do not overlap (each writer its own, the stride-2 phase launches of
+    one layer one shared region)."""
+    hr = make().coarse_model
+    g = hr._lower(E.Graph(torch.bfloat16), 32, 256)
+    plan = g.compile(2, torch.device("cpu"), backward=True)
+    kinds = [plan.bwd_arr[i].kind for i in range(plan.n_bwd)]
+    assert L.OP_WREDUCE not in kinds and kinds.count(L.OP_WREDUCE_MULTI) >= 5
+    n_red = 0
+    for i, k in enumerate(kinds):
+        if k == L.OP_WREDUCE_MULTI:
+            m = plan.bwd_arr[i].u.wreduce_multi
+            assert 1 <= m.n <= 16
+            n_red += m.n
+    assert n_red == sum(1 for s in plan._grad_slots if s[2] != "bn")
+    for idx, lay, which, first in plan._grad_slots:
+        assert isinstance(idx, tuple) and kinds[idx[1]] == L.OP_WREDUCE_MULTI
+    comp = [c for c, _ in plan.completions]
+    assert comp == sorted(comp) and all(kinds[c - 1] == L.OP_WREDUCE_MULTI for c in comp)
+    # the slab ranges the reductions of one batch read from the shared workspace are disjoint
+    ws0, ws1 = plan.ws.data_ptr(), plan.ws.data_ptr() + 4 * plan.ws.numel()
+    for i, k in enumerate(kinds):
+        if k != L.OP_WREDUCE_MULTI:
+            continue
+        m = plan.bwd_arr[i].u.wreduce_multi
+        descs = (L.WreduceDesc * m.n).from_address(m.descs)
+        rs = sorted((d.ws, d.ws + 4 * d.splits * d.ws_rows * d.ws_k) for d in descs if ws0 <= d.ws < ws1)
+        assert all(a[1] <= b[0] for a, b in zip(rs, rs[1:])), rs
+        assert all(e <= ws1 for _, e in rs)
 
 
 def test_fused_segenc_backward_leaves_no_dead_work():
