@@ -420,6 +420,71 @@ __global__ __launch_bounds__(256) void ew_fuse2_kernel(const dvie_ew_desc p, int
   if (two) finish(x + 1, v1);
 }
 
+// EW_FUSE of ONE source upsampled by an integer ratio R (align_corners False; HRNet's fuse
+// and concat upsamples, R = 2 / 4), bf16 x8: a thread owns the R output columns R q .. R q + R - 1
+// of one output row, whose bilinear columns all lie in {q - 1, q, q + 1}: 2 rows x 3 column
+// loads per R outputs (ew_fuse2_kernel: 6 per 2).  Per output the lerp indices, weights and
+// arithmetic are up_sample_add's (lerp_src), so the results are the same as ew_kernel's.
+template <int R>
+__global__ __launch_bounds__(256) void ew_fuser_kernel(const dvie_ew_desc p, int cq) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int sw = p.sw0, sh = p.sh0;
+  if (e >= sw * cq) return;
+  const int q = e / cq;
+  const int c = (e - q * cq) * 8;
+  const int row = blockIdx.y;
+  const int n = row / p.h, y = row - (row / p.h) * p.h;
+  const bf16_t* s = (const bf16_t*)p.src0;
+  const long long ld = p.src_ld0;
+  const Lerp ly = lerp_src(y, sh, p.h, 0);
+  const long long r0 = ((long long)n * sh + ly.i0) * sw, r1 = ((long long)n * sh + ly.i1) * sw;
+  const int qm = q > 0 ? q - 1 : 0, qp = q + 1 < sw ? q + 1 : sw - 1;
+  float tm0[8], t00[8], tp0[8], tm1[8], t01[8], tp1[8];
+  VecN<bf16_t, 8>::load(s + (r0 + qm) * ld + c, tm0);
+  VecN<bf16_t, 8>::load(s + (r0 + q) * ld + c, t00);
+  VecN<bf16_t, 8>::load(s + (r0 + qp) * ld + c, tp0);
+  VecN<bf16_t, 8>::load(s + (r1 + qm) * ld + c, tm1);
+  VecN<bf16_t, 8>::load(s + (r1 + q) * ld + c, t01);
+  VecN<bf16_t, 8>::load(s + (r1 + qp) * ld + c, tp1);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int x = R * q + r;
+    if (x >= p.w) break;
+    const Lerp lx = lerp_src(x, sw, p.w, 0);  // lx.i0 in {q - 1, q}, lx.i1 in {q, q + 1}
+    const bool lo = lx.i0 < q, hi = lx.i1 > q;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = lo ? tm0[k] : t00[k], b = hi ? tp0[k] : t00[k];
+      const float cc = lo ? tm1[k] : t01[k], d = hi ? tp1[k] : t01[k];
+      v[k] = 0.f + (ly.l0 * (lx.l0 * a + lx.l1 * b) + ly.l1 * (lx.l0 * cc + lx.l1 * d));
+    }
+    const long long pix = (long long)row * p.w + x;
+    bf16_t* yp = (bf16_t*)p.y + pix * p.y_ld + c;
+    float t[8];
+    if (p.res) {
+      VecN<bf16_t, 8>::load((const bf16_t*)p.res + pix * p.res_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (p.beta) {
+      VecN<bf16_t, 8>::load(yp, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (p.act) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd(v[k], p.act, p.alpha);
+    }
+    if (p.dact) {
+      VecN<bf16_t, 8>::load((const bf16_t*)p.z + pix * p.z_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= act_dz(t[k], p.dact, p.alpha);
+    }
+    VecN<bf16_t, 8>::store(yp, v);
+  }
+}
+
 // EW_UPT (the upsample adjoint) at an integer ratio R (align_corners False), bf16 x8, with two
 // horizontally adjacent coarse outputs per thread: their fine-column windows (2R + 2 each,
 // R apart) overlap, so a fine row costs 3R + 2 loads per pair instead of 4R + 4.  Same
@@ -573,6 +638,12 @@ static bool fuse2_on() {
   return !(e && *e == '0');
 }
 
+// DVIE_EW_FUSER=0: single-source integer-ratio fuse ops on ew_fuse2_kernel (A/B runs)
+static bool fuser_on() {
+  const char* e = getenv("DVIE_EW_FUSER");
+  return !(e && *e == '0');
+}
+
 // DVIE_EW_UPT2=0: one coarse output per thread for the integer-ratio upsample adjoint (A/B)
 static bool upt2_on() {
   const char* e = getenv("DVIE_EW_UPT2");
@@ -609,6 +680,13 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
       if (d->op == DVIE_EW_NCHW && !d->res && !d->beta && !d->act && !d->dact) {
         const dim3 gn((unsigned)((d->w + 255) / 256), (unsigned)(d->n * d->h));
         DVIE_LAUNCH(ew_nchw_kernel, gn, dim3(256), 0, s, *d);
+      } else if (d->op == DVIE_EW_FUSE && d->nsrc == 1 && !d->align && fuser_on() &&
+                 ((d->h == 4 * d->sh0 && d->w == 4 * d->sw0) || (d->h == 2 * d->sh0 && d->w == 2 * d->sw0))) {
+        const dim3 gr((unsigned)((d->sw0 * cq + 255) / 256), (unsigned)(d->n * d->h));
+        if (d->w == 4 * d->sw0)
+          DVIE_LAUNCH((ew_fuser_kernel<4>), gr, dim3(256), 0, s, *d, cq);
+        else
+          DVIE_LAUNCH((ew_fuser_kernel<2>), gr, dim3(256), 0, s, *d, cq);
       } else if (d->op == DVIE_EW_FUSE && up && fuse2_on()) {
         const dim3 g2((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * d->h));
         DVIE_LAUNCH((ew_fuse2_kernel<bf16_t, 8>), g2, dim3(256), 0, s, *d, cq);

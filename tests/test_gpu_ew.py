@@ -86,6 +86,45 @@ def test_fuse_upsample(dev, case, pairs, monkeypatch):
     assert err < 1e-2, (case, err)
 
 
+R_CASES = [(2, 64, 128, 16, 32, 64), (2, 64, 128, 32, 64, 32), (1, 48, 80, 12, 20, 256), (1, 40, 72, 20, 36, 128)]
+
+
+@pytest.mark.parametrize("case", R_CASES)
+def test_fuse_single_source_integer_ratio(dev, case, monkeypatch):
+    """EW_FUSE of ONE source upsampled 2x / 4x (HRNet's concat and fuse upsamples) on
+    ew_fuser_kernel (R outputs per thread), into a channel slice of a wider buffer with an
+    accumulate + LeakyReLU-derivative epilogue: equal to ew_fuse2_kernel's result bit for bit
+    (same lerp arithmetic per output) and to torch within the bf16 bar."""
+    n, H, W, h, w, c = case
+    g = torch.Generator().manual_seed(9)
+    x1 = _bf(torch.randn(n, h, w, c, generator=g))
+    y0 = _bf(torch.randn(n, H, W, c, generator=g))
+    z = _bf(torch.randn(n, H, W, c, generator=g))
+    ref = F.interpolate(x1.permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=False).permute(0, 2, 3, 1)
+    ref = (ref + y0) * torch.where(z > 0, 1.0, 0.2)
+    outs = {}
+    for tag, env in (("r", "1"), ("pair", "0")):
+        monkeypatch.setenv("DVIE_EW_FUSER", env)
+        yb = torch.zeros(n, H, W, c + 24, dtype=torch.bfloat16, device=dev)
+        yb[..., 8:8 + c] = y0.to(torch.bfloat16)
+        src = x1.to(torch.bfloat16).to(dev)
+        zd = z.to(torch.bfloat16).to(dev)
+        d = _desc(L.EW_FUSE, n, H, W, c, yb[..., 8:], c + 24)
+        d.nsrc, d.align, d.beta, d.dact, d.z, d.z_ld = 1, 0, 1, L.ACT_LRELU, zd.data_ptr(), c
+        d.src0, d.src_ld0, d.sh0, d.sw0 = src.data_ptr(), c, h, w
+        L.load().dvie_trace_kernels(1)
+        _run(d)
+        names = L.load().dvie_traced_kernels().decode()
+        L.load().dvie_trace_kernels(0)
+        assert ("ew_fuser_kernel" in names) == (tag == "r"), names
+        outs[tag] = yb.cpu()
+    assert torch.equal(outs["r"], outs["pair"])
+    got = outs["r"][..., 8:8 + c].float()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2, (case, err)
+    assert not bool(outs["r"][..., :8].any()) and not bool(outs["r"][..., 8 + c:].any())
+
+
 @pytest.mark.parametrize("c", [24, 40])
 @pytest.mark.parametrize("norm", [False, True])
 def test_nchw_pack(dev, norm, c):
