@@ -579,6 +579,112 @@ __global__ __launch_bounds__(256) void ew_upt2_kernel(const dvie_ew_desc p, int 
   if (two) finish(x + 1, v1);
 }
 
+// EW_UPT at an integer ratio R (align_corners False), bf16 x8, 2 x 2 coarse outputs per thread
+// (coarse rows y, y + 1, columns x, x + 1): the fine pixels reaching coarse i are exactly
+// R i - R/2 .. R i + R + R/2 - 1 per axis (the forward's lerp; edge clamping keeps them inside),
+// so the four outputs read one 3R x 3R fine box: (3R)^2 / 4 loads per output (R = 4: 36, against
+// 80 for upt_ratio's 2R + 2 candidates; R = 2: 9 against ew_upt2_kernel's 16).  Separable: each
+// fine row is first combined across the columns (weights upt_weight, as the forward), then
+// added into the rows' outputs with the row weights.  fp32 accumulation; the summation order
+// differs from upt_ratio's (row partials first), so results agree to fp32 rounding.
+template <int R>
+__global__ __launch_bounds__(256) void ew_upt22_kernel(const dvie_ew_desc p, int cq) {
+  constexpr int NW = 3 * R;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int wp = (p.w + 1) >> 1, hp = (p.h + 1) >> 1;
+  if (e >= wp * cq) return;
+  const int xp = e / cq;
+  const int c = (e - xp * cq) * 8;
+  const int x = 2 * xp;
+  const int rowp = blockIdx.y;
+  const int n = rowp / hp, y = 2 * (rowp - (rowp / hp) * hp);
+  const bool twox = x + 1 < p.w, twoy = y + 1 < p.h;
+  const int sh = p.sh0, sw = p.sw0;
+  const long long ld = p.src_ld0;
+  const int Y0 = R * y - R / 2, X0 = R * x - R / 2;
+  float wx0[NW], wx1[NW];
+  unsigned xo[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int X = X0 + j;
+    const bool in = X >= 0 && X < sw;
+    wx0[j] = in ? upt_weight(X, x, p.w, sw, 0) : 0.f;
+    wx1[j] = (in && twox) ? upt_weight(X, x + 1, p.w, sw, 0) : 0.f;
+    xo[j] = (unsigned)((in ? X : 0) * ld + c) * 2u;
+  }
+  // (32-bit buffer offsets: the launch checks the source span < 2 GB)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.src0, 0, 0x7FFFFFF0, 0x00020000);
+  float acc[2][2][8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[a][b][k] = 0.f;
+#pragma unroll 1
+  for (int i = 0; i < NW; ++i) {
+    const int Y = Y0 + i;
+    if (Y < 0 || Y >= sh) continue;
+    const float wy0 = upt_weight(Y, y, p.h, sh, 0), wy1 = twoy ? upt_weight(Y, y + 1, p.h, sh, 0) : 0.f;
+    if (wy0 == 0.f && wy1 == 0.f) continue;
+    const unsigned rowo = (unsigned)(((long long)n * sh + Y) * sw * ld) * 2u;
+    i32x4 raw[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) raw[j] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, rowo + xo[j], 0, 0));
+    float h0[8], h1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h0[k] = h1[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NW; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = __uint_as_float(((uint32_t)raw[j][k]) << 16), hi = __uint_as_float(((uint32_t)raw[j][k]) & 0xffff0000u);
+        h0[2 * k] += wx0[j] * lo;
+        h0[2 * k + 1] += wx0[j] * hi;
+        h1[2 * k] += wx1[j] * lo;
+        h1[2 * k + 1] += wx1[j] * hi;
+      }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      acc[0][0][k] += wy0 * h0[k];
+      acc[0][1][k] += wy0 * h1[k];
+      acc[1][0][k] += wy1 * h0[k];
+      acc[1][1][k] += wy1 * h1[k];
+    }
+  }
+  auto finish = [&](int yy, int xx, float* v) {
+    const long long pix = ((long long)n * p.h + yy) * p.w + xx;
+    bf16_t* yp = (bf16_t*)p.y + pix * p.y_ld + c;
+    float t[8];
+    if (p.res) {
+      VecN<bf16_t, 8>::load((const bf16_t*)p.res + pix * p.res_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (p.beta) {
+      VecN<bf16_t, 8>::load(yp, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += t[k];
+    }
+    if (p.act) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_fwd(v[k], p.act, p.alpha);
+    }
+    if (p.dact) {
+      VecN<bf16_t, 8>::load((const bf16_t*)p.z + pix * p.z_ld + c, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= act_dz(t[k], p.dact, p.alpha);
+    }
+    VecN<bf16_t, 8>::store(yp, v);
+  };
+  finish(y, x, acc[0][0]);
+  if (twox) finish(y, x + 1, acc[0][1]);
+  if (twoy) {
+    finish(y + 1, x, acc[1][0]);
+    if (twox) finish(y + 1, x + 1, acc[1][1]);
+  }
+}
+
 // EW_NCHW for bf16 x8 without epilogue operands: one PIXEL per thread, consecutive threads on
 // consecutive x, so every planar read (one channel of 64 pixels per wave) is a contiguous
 // 256-B row piece -- the generic kernel's channel-fastest mapping made them 4-byte gathers
@@ -638,9 +744,16 @@ static bool fuse2_on() {
   return !(e && *e == '0');
 }
 
-// DVIE_EW_FUSER=0: single-source integer-ratio fuse ops on ew_fuse2_kernel (A/B runs)
-static bool fuser_on() {
+// DVIE_EW_FUSER: single-source integer-ratio fuse ops on ew_fuser_kernel -- 1 (default) at
+// ratio 4, 2 at ratios 2 and 4, 0 never (A/B runs)
+static int fuser_on() {
   const char* e = getenv("DVIE_EW_FUSER");
+  return e && *e ? atoi(e) : 1;
+}
+
+// DVIE_EW_UPT22=0: the integer-ratio upsample adjoint without the 2 x 2-output kernel (A/B)
+static bool upt22_on() {
+  const char* e = getenv("DVIE_EW_UPT22");
   return !(e && *e == '0');
 }
 
@@ -681,7 +794,9 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
         const dim3 gn((unsigned)((d->w + 255) / 256), (unsigned)(d->n * d->h));
         DVIE_LAUNCH(ew_nchw_kernel, gn, dim3(256), 0, s, *d);
       } else if (d->op == DVIE_EW_FUSE && d->nsrc == 1 && !d->align && fuser_on() &&
-                 ((d->h == 4 * d->sh0 && d->w == 4 * d->sw0) || (d->h == 2 * d->sh0 && d->w == 2 * d->sw0))) {
+                 ((d->h == 4 * d->sh0 && d->w == 4 * d->sw0) || (fuser_on() > 1 && d->h == 2 * d->sh0 && d->w == 2 * d->sw0))) {
+        // ratio 4 only by default: the 4x 256-channel concat upsample 0.190 -> 0.167 ms/step, while
+        // at ratio 2 the pair kernel measured faster (0.092 vs 0.097 ms, profiles/r06/ew_ab_*)
         const dim3 gr((unsigned)((d->sw0 * cq + 255) / 256), (unsigned)(d->n * d->h));
         if (d->w == 4 * d->sw0)
           DVIE_LAUNCH((ew_fuser_kernel<4>), gr, dim3(256), 0, s, *d, cq);
@@ -692,7 +807,15 @@ extern "C" int dvie_ew(const dvie_ew_desc* d, void* stream) {
         DVIE_LAUNCH((ew_fuse2_kernel<bf16_t, 8>), g2, dim3(256), 0, s, *d, cq);
       } else if (d->op == DVIE_EW_FUSE)
         DVIE_LAUNCH((ew_kernel<bf16_t, 8, DVIE_EW_FUSE>), grid, dim3(256), 0, s, *d, cq);
-      else if (d->op == DVIE_EW_UPT && !d->align && upt2_on() &&
+      else if (d->op == DVIE_EW_UPT && !d->align && upt22_on() &&
+               (unsigned long long)d->n * d->sh0 * d->sw0 * d->src_ld0 * 2ull < 0x7FFFFFF0ull &&
+               ((d->sh0 == 2 * d->h && d->sw0 == 2 * d->w) || (d->sh0 == 4 * d->h && d->sw0 == 4 * d->w))) {
+        const dim3 g4((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * ((d->h + 1) / 2)));
+        if (d->sh0 == 4 * d->h)
+          DVIE_LAUNCH((ew_upt22_kernel<4>), g4, dim3(256), 0, s, *d, cq);
+        else
+          DVIE_LAUNCH((ew_upt22_kernel<2>), g4, dim3(256), 0, s, *d, cq);
+      } else if (d->op == DVIE_EW_UPT && !d->align && upt2_on() &&
                (unsigned long long)d->n * d->sh0 * d->sw0 * d->src_ld0 * 2ull < 0x7FFFFFF0ull &&
                (d->sh0 == 2 * d->h && d->sw0 == 2 * d->w)) {
         const dim3 g2((unsigned)((((d->w + 1) / 2) * cq + 255) / 256), (unsigned)(d->n * d->h));

@@ -103,7 +103,7 @@ def test_fuse_single_source_integer_ratio(dev, case, monkeypatch):
     ref = F.interpolate(x1.permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=False).permute(0, 2, 3, 1)
     ref = (ref + y0) * torch.where(z > 0, 1.0, 0.2)
     outs = {}
-    for tag, env in (("r", "1"), ("pair", "0")):
+    for tag, env in (("r", "2"), ("pair", "0")):
         monkeypatch.setenv("DVIE_EW_FUSER", env)
         yb = torch.zeros(n, H, W, c + 24, dtype=torch.bfloat16, device=dev)
         yb[..., 8:8 + c] = y0.to(torch.bfloat16)
