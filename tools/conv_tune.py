@@ -30,6 +30,11 @@ SHAPES = [  # name, cin, cout, k, H, W, batch
     ("3x3 32->32 256x512", 32, 32, 3, 256, 512, 8),
     ("3x3 24->64 256x512", 24, 64, 3, 256, 512, 8),
     ("3x3 8->448 256x512", 8, 448, 3, 256, 512, 8),
+    # VGG19's deep blocks (data gradients run on the 8 predicted frames, forwards on 16)
+    ("3x3 512->512 16x32 b8", 512, 512, 3, 16, 32, 8),
+    ("3x3 512->512 16x32 b16", 512, 512, 3, 16, 32, 16),
+    ("3x3 512->512 32x64 b8", 512, 512, 3, 32, 64, 8),
+    ("3x3 512->256 32x64 b8", 512, 256, 3, 32, 64, 8),
 ]
 
 
