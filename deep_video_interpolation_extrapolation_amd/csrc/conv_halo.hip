@@ -1769,6 +1769,10 @@ bool conv_halo_launch(const dvie_conv_desc& p, hipStream_t s) {
       cfg = p.cout <= 64 ? 3 : (p.c <= 64 ? 5 : 4);
     else
       cfg = (p.cout <= 64 || p.cout % 128 != 0) ? 3 : 4;
+    // fewer 4-row tiles than CUs (VGG19's deep data gradients on 8 frames, 512 -> 512 at
+    // 16 x 32 and 512 -> 256 at 32 x 64): 2-row tiles of the same 128 channels fill the chip,
+    // 52.9 -> 40.9 and 55.5 -> 43.5 us (profiles/r06/vgg_tune.txt)
+    if (t3 && cfg == 4 && (long long)(p.cout / 128) * ((p.ow + 63) / 64) * ((p.oh + 3) / 4) * p.n < 256) cfg = 5;
   }
   if (t3) return launch_cfg<3, 3>(cfg, p, s);
   if (t1) return launch_cfg<1, 1>(cfg, p, s);

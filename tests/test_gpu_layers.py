@@ -91,5 +91,5 @@ def test_every_op_of_the_bf16_step_matches_its_reference(dev, monkeypatch, batch
         names = " ".join(per_kernel)
         for k in ("conv_h8_kernel", "conv_strip_kernel", "conv1x1_kernel", "conv1x1_ring_kernel", "conv_s2_kernel",
                   "wgrad_halo_kernel", "wgrad_wide_kernel", "head3_bwd_kernel", "segenc_bwd_kernel", "pack_kernel",
-                  "wreduce_multi_kernel", "ew_fuse2_kernel", "ew_upt2_kernel", "ew_nchw_kernel"):
+                  "wreduce_multi_kernel", "ew_fuse2_kernel", "ew_fuser_kernel", "ew_upt22_kernel", "ew_nchw_kernel"):
             assert k in names, (k, sorted(per_kernel))
