@@ -1196,7 +1196,7 @@ struct NkCfg {
   static constexpr int NS = (NG + 1) / 2;    // 16-deep MFMA slices
 };
 
-template <int CP8, bool OUTF32>
+template <int CP8, bool OUTF32, bool PRE = false>
 __global__ __launch_bounds__(512, 2) void conv_nk_kernel(const dvie_conv_desc p, int n_cb, int n_tiles, int tiles_x,
                                                         int tiles_y) {
   typedef NkCfg<CP8> C;
@@ -1275,6 +1275,138 @@ __global__ __launch_bounds__(512, 2) void conv_nk_kernel(const dvie_conv_desc p,
   const int b_base = ((wp * C::HWD + r32) * C::PS) * 16;
   TP cur = decode(tile0);
   halo_issue(cur, 0);
+  if constexpr (PRE) {
+    // Epilogue operands (residual / accumulate / activation input) of the NEXT tile are loaded
+    // into registers right after this tile's stores, and every store and operand load is a
+    // buffer instruction that every wave issues (out-of-range lanes aimed past the buffer), so
+    // per tile a wave issues exactly [next halo: NPC][stores: 4][operand loads: 4 nops] and the
+    // wait before the barrier, vmcnt(4 + 4 nops), covers the halo only: the stores drain and
+    // the operands land under the next tile's MFMAs (before: the operands were loaded inside
+    // the epilogue and one vmcnt(0) per tile waited for the halo and the stores together).
+    const int co0 = cb * 64 + 32 * wc + 8 * hh;
+    const unsigned long long yspan =
+        ((unsigned long long)p.n * p.yh * p.yw - 1) * (unsigned long long)p.y_ld * 2ull + (unsigned long long)p.cout * 2ull;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.y, 0, (int)yspan, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.res, 0,
+        p.res ? (int)(((unsigned long long)p.n * p.yh * p.yw - 1) * (unsigned long long)p.res_ld * 2ull + p.cout * 2ull) : 0,
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.z, 0,
+        p.dact ? (int)(((unsigned long long)p.n * p.yh * p.yw - 1) * (unsigned long long)p.z_ld * 2ull + p.cout * 2ull) : 0,
+        0x00020000);
+    const int nops = (p.res ? 1 : 0) + (p.beta ? 1 : 0) + (p.dact ? 1 : 0);
+    // the lane's element offsets of accumulator b, pair P in the three operand images (or OOB)
+    auto offs = [&](const TP& T, int b, int P, unsigned& oy_, unsigned& or_, unsigned& oz_) {
+      const int oy = T.y0 + wp, ox = T.x0 + 32 * b + r32, co = co0 + 16 * P;
+      const bool ok = oy < p.oh && ox < p.ow && co < p.cout;
+      const long long pix = ((long long)T.n * p.yh + oy * p.osy + p.ory) * p.yw + ox * p.osx + p.orx;
+      oy_ = ok ? (unsigned)((pix * p.y_ld + co) * 2) : OOB;
+      or_ = ok ? (unsigned)((pix * p.res_ld + co) * 2) : OOB;
+      oz_ = ok ? (unsigned)((pix * p.z_ld + co) * 2) : OOB;
+    };
+    // one i32x4 per (operand, b, P); a flag-off operand is never read (its loads are not issued)
+    i32x4 er[2][2], eb[2][2], ez[2][2];
+    auto prefetch = [&](const TP& T) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          unsigned o_y, o_r, o_z;
+          offs(T, b, P, o_y, o_r, o_z);
+          if (p.res) er[b][P] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, o_r, 0, 0));
+          if (p.beta) eb[b][P] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, o_y, 0, 0));
+          if (p.dact) ez[b][P] = __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(rz, o_z, 0, 0));
+        }
+    };
+    f32x4 bia[2][2];
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      const int co = co0 + 16 * P;
+      bia[P][0] = p.bias && co < p.cout ? *(const f32x4*)(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      bia[P][1] = p.bias && co < p.cout ? *(const f32x4*)(p.bias + co + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    prefetch(cur);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    int hb = 0;
+    for (int tile = tile0; tile < n_tiles; tile += per_cb, hb ^= 1) {
+      const bool has_next = tile + per_cb < n_tiles;
+      const TP nxt = decode(has_next ? tile + per_cb : tile);
+      halo_issue(nxt, hb ^ 1);  // (a repeat of the current tile at the end: uniform counts)
+      f32x16 acc[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+      const char* H = smem + hb * C::HSZ + b_base;
+#pragma unroll
+      for (int sl = 0; sl < C::NS; ++sl) {
+        i32x4 bf[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) bf[b] = *(const i32x4*)(H + boff[sl] + 32 * b * C::PS * 16);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wa[sl]), __builtin_bit_cast(bf16x8, bf[b]),
+                                                           acc[b], 0, 0, 0);
+      }
+      // epilogue of the current tile from the prefetched operands: 4 buffer stores per wave
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float v[2][8];
+#pragma unroll
+        for (int P = 0; P < 2; ++P)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[b][8 * P + e]),
+                                                             __float_as_uint(acc[b][8 * P + 4 + e]), false, false);
+            v[P][e] = __uint_as_float(sw[0]) + bia[P][0][e];
+            v[P][4 + e] = __uint_as_float(sw[1]) + bia[P][1][e];
+          }
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          float* w = v[P];
+          if (p.res) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[2 * e] += __uint_as_float(((uint32_t)er[b][P][e]) << 16);
+              w[2 * e + 1] += __uint_as_float(((uint32_t)er[b][P][e]) & 0xffff0000u);
+            }
+          }
+          if (p.beta) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              w[2 * e] += __uint_as_float(((uint32_t)eb[b][P][e]) << 16);
+              w[2 * e + 1] += __uint_as_float(((uint32_t)eb[b][P][e]) & 0xffff0000u);
+            }
+          }
+          act_apply(w, 8, p.act, p.alpha);
+          if (p.dact) {
+            float t8[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              t8[2 * e] = __uint_as_float(((uint32_t)ez[b][P][e]) << 16);
+              t8[2 * e + 1] = __uint_as_float(((uint32_t)ez[b][P][e]) & 0xffff0000u);
+            }
+            dact_apply(w, t8, 8, p.dact, p.alpha);
+          }
+          i32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (int)pack_bf16x2(w[2 * e], w[2 * e + 1]);
+          unsigned o_y, o_r, o_z;
+          offs(cur, b, P, o_y, o_r, o_z);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), ry, o_y, 0, 0);
+        }
+      }
+      prefetch(nxt);
+      // outstanding, oldest first: [next halo][4 stores][4 nops operand loads]
+      wait_vmcnt(4 + 4 * nops);
+      __builtin_amdgcn_s_barrier();
+      cur = nxt;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    return;
+  }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   int hb = 0;
@@ -1307,6 +1439,13 @@ __global__ __launch_bounds__(512, 2) void conv_nk_kernel(const dvie_conv_desc p,
   }
 }
 
+// DVIE_NK_PRE=0: the narrow-input kernel loads its epilogue operands inside the epilogue
+// (A/B runs); read per launch
+static bool nk_pre_on() {
+  const char* e = getenv("DVIE_NK_PRE");
+  return !(e && *e == '0');
+}
+
 template <int CP8>
 static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
   typedef NkCfg<CP8> C;
@@ -1318,8 +1457,15 @@ static void launch_nk(const dvie_conv_desc& p, hipStream_t s) {
   if (per_cb < 1) per_cb = 1;
   if (per_cb > n_tiles) per_cb = n_tiles;
   const int grid = per_cb * n_cb;
+  const unsigned long long opix = (unsigned long long)p.n * p.yh * p.yw - 1;
+  const bool spans_ok = (opix * p.y_ld + p.cout) * 2ull < 0xFFFFFF00ull &&
+                        (!p.res || (opix * p.res_ld + p.cout) * 2ull < 0xFFFFFF00ull) &&
+                        (!p.dact || (opix * p.z_ld + p.cout) * 2ull < 0xFFFFFF00ull);
   if (p.out_f32)
     DVIE_LAUNCH((conv_nk_kernel<CP8, true>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
+  else if (nk_pre_on() && spans_ok && (p.res || p.beta || p.dact))  // (no operands: the seg encoder's
+    // 20 -> 32 forward measured 0.136 -> 0.142 ms with the prefetch form, profiles/r06/nkpre_*)
+    DVIE_LAUNCH((conv_nk_kernel<CP8, false, true>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
   else
     DVIE_LAUNCH((conv_nk_kernel<CP8, false>), dim3(grid), dim3(512), 0, s, p, n_cb, n_tiles, tiles_x, tiles_y);
 }

@@ -44,7 +44,7 @@ def _lrelu(v):
     return torch.where(v > 0, v, 0.2 * v)
 
 
-def _run(dev, shape, mode, out_f32=False):
+def _run(dev, shape, mode, out_f32=False, ret_out=False):
     n, H, W, c, cout, k = shape
     g = torch.Generator().manual_seed(7)
     x = _bf(torch.randn(n, H, W, c, generator=g))
@@ -92,7 +92,8 @@ def _run(dev, shape, mode, out_f32=False):
             "conv")
     torch.cuda.synchronize()
     out = yd.float().cpu()
-    return float((out - ref).abs().max() / ref.abs().max())
+    err = float((out - ref).abs().max() / ref.abs().max())
+    return (err, out) if ret_out else err
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -100,6 +101,28 @@ def _run(dev, shape, mode, out_f32=False):
 def test_conv_epilogue_operands(dev, shape, mode):
     err = _run(dev, shape, mode)
     assert err < 1e-2, (shape, mode, err)
+
+
+NK_SHAPES = [  # 3x3 dense-K (c <= 24): the seg head's data-gradient shape and the stems, ragged
+    (2, 35, 90, 24, 448, 3),    # 7 output blocks of 64
+    (1, 37, 70, 8, 448, 3),
+    (2, 40, 70, 16, 64, 3),
+    (1, 9, 33, 24, 96, 3),      # one tile per output block, a partial block
+]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("shape", NK_SHAPES)
+def test_conv_nk_prefetch_bit_exact(dev, shape, mode, monkeypatch):
+    """Dense-K kernel with the next tile's epilogue operands prefetched into registers and
+    buffer stores (DVIE_NK_PRE=1, the default) against the in-epilogue loads (0): the same
+    arithmetic in the same order, so the outputs are equal; both within the fp32 bar."""
+    outs = {}
+    for pre in ("1", "0"):
+        monkeypatch.setenv("DVIE_NK_PRE", pre)
+        err, outs[pre] = _run(dev, shape, mode, ret_out=True)
+        assert err < 1e-2, (shape, mode, pre, err)
+    assert torch.equal(outs["1"], outs["0"]), (shape, mode)
 
 
 STRIP_SHAPES = [  # 3x3, c and cout <= 64, >= 65536 output pixels: the weight-stationary family
