@@ -15,7 +15,8 @@ namespace dvie {
 __device__ __forceinline__ float linspace_pm1(int i, int n) {
   if (n <= 1) return -1.f;
   const float step = 2.f / (float)(n - 1);
-  return (i < n / 2) ? -1.f + step * (float)i : 1.f - step * (float)(n - 1 - i);
+  // one rounding per half, as torch.linspace's CPU kernel (bit-equal at every size checked)
+  return (i < n / 2) ? __builtin_fmaf(step, (float)i, -1.f) : __builtin_fmaf(-step, (float)(n - 1 - i), 1.f);
 }
 
 __device__ __forceinline__ float unnorm(float g, int size, int ac) {
