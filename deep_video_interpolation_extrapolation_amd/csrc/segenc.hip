@@ -16,7 +16,10 @@
 // others read a clamped row and are discarded), B = the source image at the tap's shift
 // (8 consecutive channels of one pixel per lane).  Epilogue: permlane32 pairing gives a lane 8
 // consecutive channels of one pixel, + bias, ELU, bf16.
+#include <stdlib.h>
+
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -55,8 +58,10 @@ __device__ __forceinline__ uint32_t se_pack(float a, float b) {
 
 // One conv stage over a flattened region of `npx` pixels of width RW: output pixel q = (r, c)
 // reads the source region (width RW + 2, pitch SP, CPT 16-B chunks per pixel) at (r + i, c + j).
-// Each wave takes 32-pixel blocks round-robin; `epi(q, lane_channels, v[8])` consumes the
-// 8 consecutive channels 16 P + 8 hh .. +7 (P = 0, 1) of pixel q.
+// Each wave takes 32-pixel blocks round-robin, two at a time (blocks blk and blk + NW: the
+// weight fragment of a k-step serves both and their MFMA chains interleave); `epi(q,
+// lane_channels, v[8])` consumes the 8 consecutive channels 16 P + 8 hh .. +7 (P = 0, 1) of
+// pixel q.
 template <int KS, int CPT, int RW, int SP, int WP, typename Epi>
 __device__ __forceinline__ void se_stage(const char* Wl, int wrows, const char* Src, int npx, int wave, int lane,
                                          Epi&& epi) {
@@ -65,35 +70,53 @@ __device__ __forceinline__ void se_stage(const char* Wl, int wrows, const char* 
   const int r32 = lane & 31, hh = lane >> 5;
   const char* Wa = Wl + (r32 < wrows ? r32 : r32 & (wrows - 1)) * WP + hh * 16;
   const int nblk = (npx + 31) / 32;
-  for (int blk = wave; blk < nblk; blk += SeCfg::NW) {
-    const int q = blk * 32 + r32;
-    const int qc = q < npx ? q : npx - 1;  // (pad lanes read a valid pixel, results dropped)
-    const int r = qc / RW, c = qc - r * RW;
-    const char* B = Src + (r * SW + c) * SP;
-    f32x16 acc;
+  auto run = [&](int blk0, auto nbt) {
+    constexpr int NB = decltype(nbt)::value;
+    int q[NB];
+    const char* B[NB];
+    f32x16 acc[NB];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    for (int b = 0; b < NB; ++b) {
+      q[b] = (blk0 + SeCfg::NW * b) * 32 + r32;
+      const int qc = q[b] < npx ? q[b] : npx - 1;  // (pad lanes read a valid pixel, results dropped)
+      const int r = qc / RW, c = qc - r * RW;
+      B[b] = Src + (r * SW + c) * SP;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
+    }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const i32x4 a = *(const i32x4*)(Wa + s * 32);
       int kc = 2 * s + hh;
       kc = kc < KC ? kc : KC - 1;  // zero-weight padding chunk: any finite source
       const int t = kc / CPT, cc = kc - t * CPT;
-      const i32x4 b = *(const i32x4*)(B + ((t / 3) * SW + t % 3) * SP + cc * 16);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc,
-                                                    0, 0, 0);
-    }
-    float v[2][8];
 #pragma unroll
-    for (int P = 0; P < 2; ++P)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[8 * P + e]),
-                                                         __float_as_uint(acc[8 * P + 4 + e]), false, false);
-        v[P][e] = __uint_as_float(sw[0]);
-        v[P][4 + e] = __uint_as_float(sw[1]);
+      for (int b = 0; b < NB; ++b) {
+        const i32x4 bv = *(const i32x4*)(B[b] + ((t / 3) * SW + t % 3) * SP + cc * 16);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bv),
+                                                         acc[b], 0, 0, 0);
       }
-    if (q < npx) epi(q / RW, q % RW, v);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      float v[2][8];
+#pragma unroll
+      for (int P = 0; P < 2; ++P)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[b][8 * P + e]),
+                                                           __float_as_uint(acc[b][8 * P + 4 + e]), false, false);
+          v[P][e] = __uint_as_float(sw[0]);
+          v[P][4 + e] = __uint_as_float(sw[1]);
+        }
+      if (q[b] < npx) epi(q[b] / RW, q[b] % RW, v);
+    }
+  };
+  for (int blk = wave; blk < nblk; blk += 2 * SeCfg::NW) {
+    if (blk + SeCfg::NW < nblk)
+      run(blk, std::integral_constant<int, 2>());
+    else
+      run(blk, std::integral_constant<int, 1>());
   }
 }
 
@@ -318,15 +341,104 @@ static_assert(SbCfg::SMEM <= 163840, "segenc backward LDS");
 // byte offset of 16-B chunk c of pixel p in a swizzled 64-B-pitch image
 __device__ __forceinline__ int sw64(int p, int c) { return p * 64 + ((c ^ ((p >> 2) & 3)) << 4); }
 
+// Phase 3 of the backward for one wave: its NBN 32-column blocks of weight-gradient GEMM
+// GEMM (0: dW4 = dout^T (x) e2, 1: dW2 = d_e2^T (x) e1, 2: dW0 = d_e1^T (x) in) over the
+// tile's 16 K-slices of 16 pixels.  A = the output-gradient image (rows o, 8 consecutive
+// pixels per lane via two transposed reads), B = the input image at the tap's shift (columns
+// n = t * cin + ci).  The lane's tap / channel of each block does not depend on the slice, so
+// it is formed once; the next slice's fragments are read while the current slice's MFMAs run
+// (one LDS round trip per slice instead of one per MFMA).
+template <int GEMM, int NBN>
+__device__ __forceinline__ void segenc_wg_phase(const char* smem, int nb0, f32x16 (&acc)[4], float& bsum, int g4, int qq,
+                                                int pq) {
+  typedef SbCfg C;
+  constexpr int CIN = GEMM == 2 ? 24 : 32;
+  int o0 = 16 * (g4 & 1) + 4 * pq;
+  // (opaque per call: keeps the compiler from hoisting this phase's address arithmetic out of
+  // the tile loop, where it would be held -- and spilled -- across the other phases)
+  asm volatile("" : "+v"(o0));
+  int tpo[NBN], cio[NBN];
+#pragma unroll
+  for (int j = 0; j < NBN; ++j) {
+    const int n0 = 32 * (nb0 + j) + o0;
+    int tp = n0 / CIN;
+    cio[j] = n0 - tp * CIN;
+    tp = tp < 9 ? tp : 8;  // columns past 9 cin: finite data, discarded
+    tpo[j] = (tp / 3) * C::E_W + tp % 3;
+  }
+  // A row of the tile is 4 slices; within it the lane's fragments of slice k sit 16 pixels
+  // past those of slice k - 1 in every image (the 64-B swizzle repeats every 4 pixels), so the
+  // addresses are formed once per row and the slices read at immediate offsets
+  constexpr int ASTEP = GEMM == 0 ? 16 * 16 : 16 * 64;
+  constexpr int BSTEP = GEMM == 2 ? 16 * 48 : 16 * 64;
+  struct Addr {
+    const char *a0, *a1, *b0[NBN], *b1[NBN];
+  };
+  auto base = [&](int row) {
+    Addr A;
+    const int cc = 8 * (g4 >> 1) + qq;  // the lane's tile pixel in slice 0 of the row (+ 4 for the second read)
+    const int pb = row * C::E_W + cc;   // the tile pixel in the 66-wide images, tap (0, 0)
+    if constexpr (GEMM == 0) {  // dout rows o = o0 .. +3: rows past 7 read finite neighbours
+      A.a0 = smem + C::O_DO + ((row + 2) * C::DO_W + cc + 2) * 16 + (o0 & 7) * 2;
+      A.a1 = A.a0 + 4 * 16;
+    } else if constexpr (GEMM == 1) {
+      const int pe = pb + C::E_W + 1;
+      A.a0 = smem + C::O_D2 + sw64(pe, o0 >> 3) + (o0 & 7) * 2;
+      A.a1 = smem + C::O_D2 + sw64(pe + 4, o0 >> 3) + (o0 & 7) * 2;
+    } else {
+      const int P0 = 64 * row + cc;
+      A.a0 = smem + C::O_D1 + sw64(P0, o0 >> 3) + (o0 & 7) * 2;
+      A.a1 = smem + C::O_D1 + sw64(P0 + 4, o0 >> 3) + (o0 & 7) * 2;
+    }
+#pragma unroll
+    for (int j = 0; j < NBN; ++j) {
+      const int pe = pb + tpo[j];
+      if constexpr (GEMM == 2) {
+        A.b0[j] = smem + C::O_IN + pe * 48 + cio[j] * 2;
+        A.b1[j] = A.b0[j] + 4 * 48;
+      } else {
+        constexpr int bb = GEMM == 0 ? C::O_E2 : C::O_E1;
+        A.b0[j] = smem + bb + sw64(pe, cio[j] >> 3) + (cio[j] & 7) * 2;
+        A.b1[j] = smem + bb + sw64(pe + 4, cio[j] >> 3) + (cio[j] & 7) * 2;
+      }
+    }
+    return A;
+  };
+  auto fetch = [&](const Addr& A, int k, bf16x8& av, bf16x8 (&bv)[NBN]) {
+    av = hb_tr_pair_se(A.a0 + k * ASTEP, A.a1 + k * ASTEP);
+#pragma unroll
+    for (int j = 0; j < NBN; ++j) bv[j] = hb_tr_pair_se(A.b0[j] + k * BSTEP, A.b1[j] + k * BSTEP);
+  };
+  auto step = [&](const bf16x8& av, const bf16x8 (&bv)[NBN]) {
+#pragma unroll
+    for (int j = 0; j < NBN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[j], acc[j], 0, 0, 0);
+    // bias column sums from the A fragment: lane l holds 8 pixels of row l % 32 (the first
+    // wave of each gemm sums; every wave does the VALU work, no branch splits the k-step)
+    bsum = sum8_bf16_se(av, bsum);
+  };
+#pragma unroll 1
+  for (int row = 0; row < 4; ++row) {
+    const Addr A = base(row);
+    bf16x8 a0, a1, b0[NBN], b1[NBN];
+    fetch(A, 0, a0, b0);
+    fetch(A, 1, a1, b1);
+    step(a0, b0);
+    fetch(A, 2, a0, b0);
+    step(a1, b1);
+    fetch(A, 3, a1, b1);
+    step(a0, b0);
+    step(a1, b1);
+  }
+}
+
 __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_desc p, int tiles_x, int tiles_y,
-                                                         int n_tiles) {
+                                                         int n_tiles, int dbg) {
   typedef SbCfg C;
   constexpr int NW = C::NW;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int g4 = lane >> 4, li = lane & 15, qq = li >> 2, pq = li & 3;
+  const int hh = lane >> 5;
   const unsigned OOB = 0xFFFFFFF0u;
 
   // ---- data-gradient weights into LDS, once: w4d [32 ci][80 k], w2d [32 ci][288 k] ----
@@ -401,7 +513,8 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
     for (int q = 0; q < C::PQ; ++q) {
       const int pc = wave + NW * q;
       if (pc >= C::PCS) continue;  // (wave-uniform)
-      const int v = geo[q];
+      int v = geo[q];
+      asm volatile("" : "+v"(v));  // decoded per tile, not hoisted (and spilled) out of the loop
       const int img = pc < C::DO_PC ? 0 : pc < C::DO_PC + C::E_PC ? 1 : pc < C::DO_PC + 2 * C::E_PC ? 2 : 3;
       const int org = img == 0 ? 2 : 1;
       const int iy = y0 - org + ((v >> 20) & 0xFF), ix = x0 - org + ((v >> 8) & 0xFFF);
@@ -424,80 +537,119 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
       *(i32x4*)(smem + dst + lane * 16) = stg[q];
     }
   };
-  if ((int)blockIdx.x < n_tiles) load_tile(blockIdx.x);
+  if ((int)blockIdx.x < n_tiles && !(dbg & 64)) load_tile(blockIdx.x);
 
-  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+  for (int t = blockIdx.x; t < ((dbg & 32) ? 0 : n_tiles); t += gridDim.x) {
     int n, y0, x0;
     tile_pos(t, n, y0, x0);
     __syncthreads();  // the previous tile's reads of the images are done
     store_tile();
     __syncthreads();
-    if (t + (int)gridDim.x < n_tiles) load_tile(t + gridDim.x);
+    if (t + (int)gridDim.x < n_tiles && !(dbg & 8)) load_tile(t + gridDim.x);
 
+    // the lane's fragment coordinates, opaque per tile: every phase forms its LDS addresses
+    // from them inside the tile loop instead of the compiler hoisting all of them out of it
+    // (where they were held, and spilled, across the phases)
+    int lt = lane;
+    asm volatile("" : "+v"(lt));
+    const int r32 = lt & 31, hh = lt >> 5;
+    const int g4 = lt >> 4, qq = (lt & 15) >> 2, pq = lt & 3;
     // ---- phase 1: d_e2 on the 6 x 66 region = ELU'(e2) * conv4^T(dout) ----
-    for (int blk = wave; blk < (C::E_H * C::E_W + 31) / 32; blk += NW) {
-      const int q = blk * 32 + r32;
-      const int qc = q < C::E_H * C::E_W ? q : C::E_H * C::E_W - 1;
-      const int rr = qc / C::E_W, cc = qc - rr * C::E_W;
-      const char* B = smem + C::O_DO + (rr * C::DO_W + cc) * 16;
-      f32x16 a1;
+    // (dbg: timing-only ablation bits from DVIE_SEGENC_DBG, 0 in every real run: 1 / 2 / 4 skip
+    // phase 1 / 2 / 3, 8 the tile loads, 16 the slab stores, 32 the whole tile loop, 64 the first tile's
+    // loads)
+    // A wave takes its blocks wave and wave + 8 together (13 blocks of 32 pixels): the weight
+    // fragment of a k-step serves both, and the two MFMA chains interleave.
+    auto p1_blocks = [&](auto nbt) {
+      constexpr int NB = decltype(nbt)::value;
+      constexpr int NPX = C::E_H * C::E_W;
+      int q[NB], qc[NB];
+      const char* B[NB];
+      f32x16 a1[NB];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) a1[e] = 0.f;
+      for (int b = 0; b < NB; ++b) {
+        q[b] = (wave + NW * b) * 32 + r32;
+        qc[b] = q[b] < NPX ? q[b] : NPX - 1;
+        const int rr = qc[b] / C::E_W, cc = qc[b] - rr * C::E_W;
+        B[b] = smem + C::O_DO + (rr * C::DO_W + cc) * 16;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) a1[b][e] = 0.f;
+      }
 #pragma unroll
       for (int s = 0; s < 5; ++s) {
         const i32x4 a = *(const i32x4*)(smem + C::O_W4 + r32 * C::W4_PITCH + hh * 16 + s * 32);
         int kc = 2 * s + hh;
         kc = kc < 9 ? kc : 8;
-        const i32x4 b = *(const i32x4*)(B + ((kc / 3) * C::DO_W + kc % 3) * 16);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1, 0,
-                                                     0, 0);
-      }
-      const int gy = y0 - 1 + rr, gx = x0 - 1 + cc;
-      const bool in = q < C::E_H * C::E_W && (unsigned)gy < (unsigned)p.h && (unsigned)gx < (unsigned)p.w;
 #pragma unroll
-      for (int P = 0; P < 2; ++P) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1[8 * P + e]),
-                                                           __float_as_uint(a1[8 * P + 4 + e]), false, false);
-          v[e] = __uint_as_float(sw[0]);
-          v[4 + e] = __uint_as_float(sw[1]);
+        for (int b = 0; b < NB; ++b) {
+          const i32x4 bv = *(const i32x4*)(B[b] + ((kc / 3) * C::DO_W + kc % 3) * 16);
+          a1[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bv),
+                                                          a1[b], 0, 0, 0);
         }
-        const int ch = 2 * P + hh;  // 16-B chunk: channels 8 ch .. +7
-        const i32x4 z = *(const i32x4*)(smem + C::O_E2 + sw64(qc, ch));
-        i32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float za = __uint_as_float(((uint32_t)z[e]) << 16), zb = __uint_as_float(((uint32_t)z[e]) & 0xffff0000u);
-          o[e] = (int)se_pack(in ? v[2 * e] * act_dz(za, DVIE_ACT_ELU, 0.f) : 0.f,
-                              in ? v[2 * e + 1] * act_dz(zb, DVIE_ACT_ELU, 0.f) : 0.f);
-        }
-        if (q < C::E_H * C::E_W) *(i32x4*)(smem + C::O_D2 + sw64(q, ch)) = o;
       }
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int rr = qc[b] / C::E_W, cc = qc[b] - rr * C::E_W;
+        const int gy = y0 - 1 + rr, gx = x0 - 1 + cc;
+        const bool in = q[b] < NPX && (unsigned)gy < (unsigned)p.h && (unsigned)gx < (unsigned)p.w;
+#pragma unroll
+        for (int P = 0; P < 2; ++P) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1[b][8 * P + e]),
+                                                             __float_as_uint(a1[b][8 * P + 4 + e]), false, false);
+            v[e] = __uint_as_float(sw[0]);
+            v[4 + e] = __uint_as_float(sw[1]);
+          }
+          const int ch = 2 * P + hh;  // 16-B chunk: channels 8 ch .. +7
+          const i32x4 z = *(const i32x4*)(smem + C::O_E2 + sw64(qc[b], ch));
+          i32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float za = __uint_as_float(((uint32_t)z[e]) << 16), zb = __uint_as_float(((uint32_t)z[e]) & 0xffff0000u);
+            o[e] = (int)se_pack(in ? v[2 * e] * act_dz(za, DVIE_ACT_ELU, 0.f) : 0.f,
+                                in ? v[2 * e + 1] * act_dz(zb, DVIE_ACT_ELU, 0.f) : 0.f);
+          }
+          if (q[b] < NPX) *(i32x4*)(smem + C::O_D2 + sw64(q[b], ch)) = o;
+        }
+      }
+    };
+    static_assert((C::E_H * C::E_W + 31) / 32 <= 2 * NW, "phase 1: two blocks per wave");
+    if (!(dbg & 1)) {
+      if (wave + NW < (C::E_H * C::E_W + 31) / 32)
+        p1_blocks(std::integral_constant<int, 2>());
+      else
+        p1_blocks(std::integral_constant<int, 1>());
     }
     __syncthreads();
 
     // ---- phase 2: d_e1 on the tile = ELU'(e1) * conv2^T(d_e2) ----
-    {
+    if (!(dbg & 2)) {
       const int blk = wave;  // 8 blocks of 32 pixels
       const int q = blk * 32 + r32, rr = q >> 6, cc = q & 63;
-      // (the K = 288 chain split over two accumulators: two independent MFMA chains)
+      // (the K = 288 chain split over two accumulators: two independent MFMA chains; the
+      // operands of k-step s + 2 are read while step s runs)
       f32x16 a1, a1b;
 #pragma unroll
       for (int e = 0; e < 16; ++e) a1[e] = a1b[e] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        const i32x4 a = *(const i32x4*)(smem + C::O_W2 + r32 * C::W2_PITCH + hh * 16 + s * 32);
+      i32x4 ra[3], rb[3];
+      auto ld2 = [&](int s, i32x4& a, i32x4& b) {
+        a = *(const i32x4*)(smem + C::O_W2 + r32 * C::W2_PITCH + hh * 16 + s * 32);
         const int kc = 2 * s + hh, tp = kc >> 2, ck = kc & 3;
         const int pe = (rr + tp / 3) * C::E_W + cc + tp % 3;
-        const i32x4 b = *(const i32x4*)(smem + C::O_D2 + sw64(pe, ck));
+        b = *(const i32x4*)(smem + C::O_D2 + sw64(pe, ck));
+      };
+      ld2(0, ra[0], rb[0]);
+      ld2(1, ra[1], rb[1]);
+#pragma unroll
+      for (int s = 0; s < 18; ++s) {
+        if (s + 2 < 18) ld2(s + 2, ra[(s + 2) % 3], rb[(s + 2) % 3]);
+        const bf16x8 av = __builtin_bit_cast(bf16x8, ra[s % 3]), bv = __builtin_bit_cast(bf16x8, rb[s % 3]);
         if (s & 1)
-          a1b = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1b,
-                                                        0, 0, 0);
+          a1b = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, a1b, 0, 0, 0);
         else
-          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), a1,
-                                                       0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, a1, 0, 0, 0);
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) a1[e] += a1b[e];
@@ -529,63 +681,30 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
     __syncthreads();
 
     // ---- phase 3: weight gradients over the tile's 256 pixels (K = pixels) ----
-    // A = output-gradient image (rows o, 8 consecutive pixels per lane via two transposed
-    // reads), B = input image at the tap's shift (columns n = t * cin + ci)
-#pragma unroll 1
-    for (int sl = 0; sl < 16; ++sl) {
-      const int P0 = 16 * sl + 8 * (g4 >> 1) + qq;  // lane's tile pixel (+ 4 for the second read)
-      const int rr = P0 >> 6, cc = P0 & 63;
-      bf16x8 av;
-      if (gemm == 0) {  // dout rows o = 16 (g4 & 1) + 4 pq .. +3: rows past 7 read finite neighbours
-        const int o0 = (16 * (g4 & 1) + 4 * pq) & 7;
-        const char* a0 = smem + C::O_DO + ((rr + 2) * C::DO_W + cc + 2) * 16 + o0 * 2;
-        av = hb_tr_pair_se(a0, a0 + 4 * 16);
-      } else if (gemm == 1) {
-        const int o0 = 16 * (g4 & 1) + 4 * pq, pe = (rr + 1) * C::E_W + cc + 1;
-        const char* a0 = smem + C::O_D2 + sw64(pe, o0 >> 3) + (o0 & 7) * 2;
-        const char* a1 = smem + C::O_D2 + sw64(pe + 4, o0 >> 3) + (o0 & 7) * 2;
-        av = hb_tr_pair_se(a0, a1);
-      } else {
-        const int o0 = 16 * (g4 & 1) + 4 * pq;
-        const char* a0 = smem + C::O_D1 + sw64(P0, o0 >> 3) + (o0 & 7) * 2;
-        const char* a1 = smem + C::O_D1 + sw64(P0 + 4, o0 >> 3) + (o0 & 7) * 2;
-        av = hb_tr_pair_se(a0, a1);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j >= nbn) break;  // (wave-uniform)
-        const int n0 = 32 * (nb0 + j) + 16 * (g4 & 1) + 4 * pq;
-        int tp = n0 / cin;
-        const int ci = n0 - tp * cin;
-        tp = tp < 9 ? tp : 8;  // columns past 9 cin: finite data, discarded
-        const int pe = (rr + tp / 3) * C::E_W + cc + tp % 3;
-        const char *b0, *b1;
-        if (gemm == 2) {
-          b0 = smem + C::O_IN + pe * 48 + ci * 2;
-          b1 = b0 + 4 * 48;
-        } else {
-          const int base = gemm == 0 ? C::O_E2 : C::O_E1;
-          b0 = smem + base + sw64(pe, ci >> 3) + (ci & 7) * 2;
-          b1 = smem + base + sw64(pe + 4, ci >> 3) + (ci & 7) * 2;
-        }
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, hb_tr_pair_se(b0, b1), acc[j], 0, 0, 0);
-      }
-      // bias column sums from the A fragment: lane l holds 8 pixels of row l % 32 (the first
-      // wave of each gemm sums; every wave does the VALU work, no branch splits the k-step)
-      bsum = sum8_bf16_se(av, bsum);
-    }
+    if (dbg & 4) {
+    } else if (gemm == 0)
+      segenc_wg_phase<0, 3>(smem, nb0, acc, bsum, g4, qq, pq);
+    else if (gemm == 1)
+      segenc_wg_phase<1, 3>(smem, nb0, acc, bsum, g4, qq, pq);
+    else if (nbn == 4)
+      segenc_wg_phase<2, 4>(smem, nb0, acc, bsum, g4, qq, pq);
+    else
+      segenc_wg_phase<2, 3>(smem, nb0, acc, bsum, g4, qq, pq);
+    // the next tile's images: issued after this tile's phases, so the 10 x 16 B per lane they
+    // land in are not held across the phases (whose MFMAs need the registers for operand
+    // pipelining); their latency is exposed once per tile at the store above
   }
 
   // ---- this workgroup's slabs ----
   const int slab = blockIdx.x;
-  {
+  if (!(dbg & 16)) {
     float* out = gemm == 0 ? p.dw4 : gemm == 1 ? p.dw2 : p.dw0;
     const int cout = gemm == 0 ? 8 : 32, kw = 9 * cin;
     out += (long long)slab * cout * kw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j >= nbn) break;
-      const int n = 32 * (nb0 + j) + r32;
+      const int n = 32 * (nb0 + j) + (lane & 31);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -619,7 +738,8 @@ extern "C" int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream) {
   const int tiles_x = (d->w + 63) / 64, tiles_y = (d->h + 3) / 4;
   const long long nt = (long long)tiles_x * tiles_y * d->n;
   DVIE_CHECK_ARG(nt < (1LL << 30), "segenc_bwd: too many tiles");
+  const char* dbg = getenv("DVIE_SEGENC_DBG");  // timing-only ablations (tools/segenc_micro.py)
   DVIE_LAUNCH(segenc_bwd_kernel, dim3(d->slabs), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y,
-                     (int)nt);
+                     (int)nt, dbg && *dbg ? atoi(dbg) : 0);
   DVIE_RETURN_LAUNCH();
 }

@@ -846,9 +846,10 @@ class Plan:
         g = self.g
         nf = self.nf
         fused_first, skip = {}, set()
-        # the fused forward measured slower than its three convs at 8x256x512 (0.555 vs 0.40 ms
-        # per step, profiles/r04e/ops.txt): opt-in (DVIE_SEGENC_FWD=1); the fused backward stays
-        fwd_on = os.environ.get("DVIE_SEGENC_FWD", "0") == "1"
+        # the fused forward (one dvie_segenc_fwd per encoder) is the default since its stages
+        # run two 32-pixel blocks per wave: 0.316 vs 0.344 ms per step for the three convs at
+        # 8x256x512 (profiles/r06/segenc_*); DVIE_SEGENC_FWD=0 runs the three convs
+        fwd_on = os.environ.get("DVIE_SEGENC_FWD", "1") == "1"
         for chain in getattr(g, "segenc", []) if fwd_on else []:
             if self._segenc_fusable(chain):
                 fused_first[id(chain[0])] = chain

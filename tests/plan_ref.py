@@ -443,6 +443,29 @@ class Interp:
                 ("dW slabs", d.ws, (d.splits, co, 9 * c), (co * 9 * c, 9 * c, 1), torch.float32, ref.reshape(co, 9 * c),
                  "slab")]
 
+    # ---------------- fused seg-encoder forward ----------------
+    def ref_segenc_fwd(self, d):
+        """e1 = ELU(conv0(in) + b0), e2 = ELU(conv2(e1) + b2), out = conv4(e2) + b4 (3x3, pad 1),
+        e1 / e2 stored bf16 and each conv reading the previous one's bf16 map (the kernel's LDS
+        images hold exactly those values)"""
+        dt = torch.bfloat16
+        n, h, w = d.n, d.h, d.w
+        geo = (h, w, 1, 1, 3, 3, -1, -1, 1, 1, dt)
+        v = self.conv_acc(d.inp, d.in_ld, n, h, w, 24, d.w0, d.kpad0, 32, *geo)
+        e1 = act_fwd(v + self.rd(d.b0, (32,), (1,), torch.float32), L.ACT_ELU, 0.0)
+        t1 = self._tmp(e1)
+        v = self.conv_acc(t1.data_ptr(), 32, n, h, w, 32, d.w2, d.kpad2, 32, *geo)
+        e2 = act_fwd(v + self.rd(d.b2, (32,), (1,), torch.float32), L.ACT_ELU, 0.0)
+        t2 = self._tmp(e2)
+        out = self.conv_acc(t2.data_ptr(), 32, n, h, w, 32, d.w4, d.kpad4, 8, *geo)
+        out = out + self.rd(d.b4, (8,), (1,), torch.float32)
+        self._tmps = []
+        e1sh, e1st = nhwc(n, h, w, d.e1_ld, 32)
+        e2sh, e2st = nhwc(n, h, w, d.e2_ld, 32)
+        osh, ost = nhwc(n, h, w, d.out_ld, 8)
+        return [("e1", d.e1, e1sh, e1st, dt, e1, "act"), ("e2", d.e2, e2sh, e2st, dt, e2, "act"),
+                ("out", d.out, osh, ost, dt, out, "act")]
+
     # ---------------- fused seg-encoder backward ----------------
     def ref_segenc_bwd(self, d):
         dt = torch.bfloat16
@@ -500,6 +523,8 @@ class Interp:
             return self.ref_head3(o.u.head3)
         if k == L.OP_SEGENC_BWD:
             return self.ref_segenc_bwd(o.u.segenc_bwd)
+        if k == L.OP_SEGENC_FWD:
+            return self.ref_segenc_fwd(o.u.segenc)
         raise NotImplementedError(f"op kind {k}")
 
 

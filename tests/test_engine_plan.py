@@ -62,11 +62,12 @@ def test_hrnet_plan_structure(dtype, fused, monkeypatch):
     # rgb output head's data + weight gradients are one fused launch (dvie_head3_bwd; the seg
     # head stays unfused by default, DVIE_HEAD3_FUSED) and each frame's segmentation encoder
     # runs its backward -- three weight gradients and two data gradients -- as one
-    # dvie_segenc_bwd launch (its forward stays three convs: DVIE_SEGENC_FWD is opt-in)
+    # dvie_segenc_bwd launch, and its forward -- three convs -- as one dvie_segenc_fwd launch
+    # (DVIE_SEGENC_FWD=0: three)
     n_head3 = 1 if dtype == torch.bfloat16 else 0
     n_seg = 2 if dtype == torch.bfloat16 else 0
     assert kinds.get(L.OP_HEAD3_BWD, 0) == n_head3
-    assert kinds.get(L.OP_SEGENC_FWD, 0) == 0 and kinds.get(L.OP_SEGENC_BWD, 0) == n_seg
+    assert kinds.get(L.OP_SEGENC_FWD, 0) == n_seg and kinds.get(L.OP_SEGENC_BWD, 0) == n_seg
     assert kinds[L.OP_WGRAD] == n_ref - n_head3 - 3 * n_seg
     n_s2 = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2)
     n_dgrad = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.x.buf.needs_grad)
@@ -76,7 +77,7 @@ def test_hrnet_plan_structure(dtype, fused, monkeypatch):
     n_ph4_want = sum(1 for op in g.ops if isinstance(op, E.ConvOp) and op.layer.stride == 2 and op.x.buf.needs_grad
                      and op.layer.cin_p <= 128) if dtype == torch.bfloat16 else 0
     assert n_ph4 == n_ph4_want
-    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * (n_s2 - n_ph4) - n_head3 - 2 * n_seg
+    assert kinds[L.OP_CONV] == n_conv_fwd + n_dgrad + 3 * (n_s2 - n_ph4) - n_head3 - 2 * n_seg - 3 * n_seg
     # every buffer that needs a gradient received all of its contributions
     for b in g.buffers:
         if b.needs_grad and b.expected:

@@ -131,7 +131,7 @@ def test_segenc_fused_forward(dev, monkeypatch):
     gr = torch.Generator().manual_seed(5)
     w1, w2 = torch.randn((2, 3, 36, 100), generator=gr), torch.randn((2, 20, 36, 100), generator=gr)
     res = {}
-    monkeypatch.setenv("DVIE_SEGENC_FWD", "1")  # the fused forward is opt-in
+    monkeypatch.setenv("DVIE_SEGENC_FWD", "1")  # the fused forward (the default)
     for mode in ("1", "0"):
         monkeypatch.setenv("DVIE_SEGENC_FUSED", mode)
         monkeypatch.setenv("DVIE_PRECISION", "bf16")

@@ -50,7 +50,7 @@ def _trainer(dev, batch, H, W):
 
 
 KIND = {1: "conv", 2: "wgrad", 3: "wreduce", 4: "colsum", 5: "ew", 6: "loss", 7: "pack", 13: "head3_bwd",
-        15: "segenc_bwd", 16: "wreduce*"}
+        14: "segenc_fwd", 15: "segenc_bwd", 16: "wreduce*"}
 
 
 @pytest.mark.parametrize("batch,H,W", [(8, 256, 512), (2, 48, 80)], ids=["c2_8x256x512", "ragged_2x48x80"])
@@ -86,10 +86,10 @@ def test_every_op_of_the_bf16_step_matches_its_reference(dev, monkeypatch, batch
     assert not chk.failures, chk.failures[:10]
     assert all(r["checked"] for r in chk.records)
     kinds = {r["kind"] for r in chk.records}
-    assert {1, 2, 5, 6, 7, 13, 15} <= kinds and (3 in kinds or 16 in kinds), kinds
+    assert {1, 2, 5, 6, 7, 13, 14, 15} <= kinds and (3 in kinds or 16 in kinds), kinds
     if (batch, H, W) == (8, 256, 512):
         names = " ".join(per_kernel)
         for k in ("conv_h8_kernel", "conv_strip_kernel", "conv1x1_kernel", "conv1x1_ring_kernel", "conv_s2_kernel",
-                  "wgrad_halo_kernel", "wgrad_wide_kernel", "head3_bwd_kernel", "segenc_bwd_kernel", "pack_kernel",
+                  "wgrad_halo_kernel", "wgrad_wide_kernel", "head3_bwd_kernel", "segenc_fwd_kernel", "segenc_bwd_kernel", "pack_kernel",
                   "wreduce_multi_kernel", "ew_fuse2_kernel", "ew_fuser_kernel", "ew_upt22_kernel", "ew_nchw_kernel"):
             assert k in names, (k, sorted(per_kernel))
