@@ -106,8 +106,8 @@ __device__ __forceinline__ float warp_blend(float a, float b, float c, float d, 
 // is a multiple of 8) workgroup b takes the job slot (b % 8) * (grid / 8) + b / 8, so each XCD
 // walks a contiguous band of rows and the source rows two neighbouring output rows share are
 // gathered into one L2 instead of two.
-template <int CC, int LAUX = 0, int SAUX = 0>
-__global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p, int xcd) {
+template <int CC, int LAUX = 0, int SAUX = 0, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void warp_fwd_kernel(const dvie_warp_desc p, int xcd) {
   const int segs = (p.w + 255) >> 8;
   const long long hw = (long long)p.h * p.w;
   const int waves = p.n * p.h * segs;  // < 2^31 (checked at launch)
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const dvie_warp_desc p, i
   const int g = gridDim.x;
   const int vb = (xcd && (g & 7) == 0) ? (int)(blockIdx.x & 7) * (g >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   // wave-uniform row/segment (readfirstlane), so the plane buffer resources are scalar
-  for (int wv = __builtin_amdgcn_readfirstlane(vb * 4 + (threadIdx.x >> 6)); wv < waves;
-       wv += gridDim.x * 4) {
+  for (int wv = __builtin_amdgcn_readfirstlane(vb * WPB + (threadIdx.x >> 6)); wv < waves;
+       wv += gridDim.x * WPB) {
     const int sg = wv % segs;
     const int r = wv / segs;
     const int y = r % p.h, n = r / p.h;
@@ -540,8 +540,14 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   DVIE_CHECK_ARG(d && d->img && d->flow && d->out && d->n > 0 && d->c > 0 && d->h > 0 && d->w > 0, "warp: args");
   const long long waves = (long long)d->n * d->h * ((d->w + 255) / 256);
   DVIE_CHECK_ARG(waves < (1LL << 31) && (long long)d->h * d->w < (1LL << 29), "warp: size");
-  // one workgroup per 4 waves (jobs) up to 8192 workgroups
-  int grid = (int)((waves + 3) / 4 < 8192 ? (waves + 3) / 4 : 8192);
+  // waves per workgroup: 8 once the frames outgrow the L2s (8x3x1024x2048: 101.5 -> 95.5 us,
+  // 0.66 -> 0.70 of HBM), 4 below (8x3x256x512: 7.5 vs 8.4 us; 16 loses at both sizes:
+  // profiles/r06/warp_wpb/).  DVIE_WARP_FWD_WPB (A/B, read per launch): 4 / 8 / 16
+  const char* we = getenv("DVIE_WARP_FWD_WPB");
+  const int wpb = we && *we ? atoi(we) : (waves >= 32768 ? 8 : 4);
+  DVIE_CHECK_ARG(wpb == 4 || wpb == 8 || wpb == 16, "warp: DVIE_WARP_FWD_WPB must be 4, 8 or 16");
+  // one workgroup per wpb waves (jobs) up to 8192 workgroups
+  int grid = (int)((waves + wpb - 1) / wpb < 8192 ? (waves + wpb - 1) / wpb : 8192);
   if (const char* e = getenv("DVIE_WARP_FWD_GRID")) {  // A/B: blocks = min(jobs / 4, cap)
     const long long need = (waves + 3) / 4, cap = atoi(e);
     if (cap > 0) grid = (int)(need < cap ? need : cap);
@@ -556,7 +562,11 @@ int dvie_warp_fwd(const dvie_warp_desc* d, void* stream) {
   // (profiles/r04aa/).  DVIE_WARP_XCD (A/B, read per launch): 1 = always, 0 = never
   const char* xe = getenv("DVIE_WARP_XCD");
   const int xcd = xe && *xe ? atoi(xe) : ((long long)d->n * d->c * d->h * d->w * 4 > (64ll << 20));
-  if (d->c == 3 && ntm == 1)
+  if (d->c == 3 && ntm == 2 && wpb == 8)
+    DVIE_LAUNCH((warp_fwd_kernel<3, 2, 2, 8>), dim3(grid), dim3(512), 0, (hipStream_t)stream, *d, xcd);
+  else if (d->c == 3 && ntm == 2 && wpb == 16)
+    DVIE_LAUNCH((warp_fwd_kernel<3, 2, 2, 16>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, *d, xcd);
+  else if (d->c == 3 && ntm == 1)
     DVIE_LAUNCH((warp_fwd_kernel<3, 0, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
   else if (d->c == 3 && ntm == 2)
     DVIE_LAUNCH((warp_fwd_kernel<3, 2, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream, *d, xcd);
