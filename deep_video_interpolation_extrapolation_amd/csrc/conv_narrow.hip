@@ -173,25 +173,35 @@ __global__ __launch_bounds__(512) void conv_narrow_kernel(const dvie_conv_desc p
     if (jj + 1 < njobs) issue(jj + 1, (jj + 1) & 1);
     const char* S = smem + (jj & 1) * C::STAGE;
     if (dbg & 2) goto skip;  // timing experiments only: no MFMAs
+    {
+      // tap t + 1's fragments are read while tap t's MFMAs run (scheduling barriers keep the
+      // compiler from interleaving each MFMA behind its own LDS round trip)
+      i32x4 fa[2][2], fb[2][2][2];
+      auto ld = [&](int t, int buf) {
+        const int ti = t / 3, tj = t % 3;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ti = t / 3, tj = t % 3;
-      int boff[2];
+        for (int s = 0; s < 2; ++s) {
+          fa[buf][s] = *(const i32x4*)(S + a_off[s] + t * 32 * C::PITCH);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int px = px0 + ti * C::HW + 32 * b + tj;
-        boff[b] = px * C::PITCH + ((hh ^ ((px >> 2) & 3)) << 4);  // k-slice s: xor 2s into the chunk
-      }
+          for (int b = 0; b < 2; ++b) {
+            const int px = px0 + ti * C::HW + 32 * b + tj;
+            const int boff = px * C::PITCH + ((hh ^ ((px >> 2) & 3)) << 4);  // k-slice s: xor 2s into the chunk
+            fb[buf][s][b] = *(const i32x4*)(S + (boff ^ (s << 5)));
+          }
+        }
+      };
+      ld(0, 0);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const i32x4 a = *(const i32x4*)(S + a_off[s] + t * 32 * C::PITCH);
-        i32x4 bq[2];
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int b = 0; b < 2; ++b) bq[b] = *(const i32x4*)(S + (boff[b] ^ (s << 5)));
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bq[b]),
-                                                           acc[b], 0, 0, 0);
+          for (int b = 0; b < 2; ++b)
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[t & 1][s]),
+                                                             __builtin_bit_cast(bf16x8, fb[t & 1][s][b]), acc[b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   skip:
