@@ -24,6 +24,8 @@
 // MFMA v_mfma_f32_32x32x16_bf16.  GEMM 1: wave (row wr, channel half wc) computes
 // dh^T[32 ch][64 px] (A = weights, B = halo).  GEMM 2: wave (ci block nb, k-row blocks mq and
 // mq + 4) over all 256 pixels of the tile.
+#include <algorithm>
+
 #include "common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -49,7 +51,12 @@ struct HbCfg {
   static constexpr int GPC = (HR * HWD * GREC / 16 + 63) / 64;
   static constexpr int GQ = (GPC + NW - 1) / NW;          // halo pieces per wave (upper bound)
   static constexpr int STAGE = HT + GPC * 1024;
-  static constexpr int SMEM = WSZ + 2 * STAGE;
+  // stage buffers: three for cout 8 (tile t + 2 streams in while tile t computes: one tile of
+  // compute did not cover a tile's DMA latency + transfer), two for cout 24 (three do not fit)
+  static constexpr int NSTG = WSZ + 3 * STAGE <= 163840 ? 3 : 2;
+  static constexpr int SMEM = WSZ + NSTG * STAGE;
+  // DMA pieces a wave issues per tile (h tile + its share of the halo)
+  __host__ __device__ static constexpr int pieces(int wave) { return HPC / NW + (wave < GPC % NW || GPC % NW == 0 ? GQ : GQ - 1); }
   // GEMM 1 B-fragment offset of k-chunk kc inside the halo (tap shift + channel chunk); the
   // zero-weight padding chunk of cout 8 reads tap 8 (finite data times zero weights)
   __host__ __device__ static constexpr int chunk_off(int kc) {
@@ -69,6 +76,23 @@ __device__ __forceinline__ bf16x8 hb_tr_pair(const char* p0, const char* p1) {
 
 __device__ __forceinline__ uint32_t hb_pack(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((hb_f32x2{a, b}), hb_bf16x2));
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n < 32 (the DMA is inline asm: the compiler counts
+// none of it, so the kernel waits for its own pieces explicitly)
+#define DVIE_HB_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (((N) >> 4) << 14) | (7 << 4) | (15 << 8))
+__device__ __forceinline__ void hb_wait_vmcnt(int n) {
+  switch (n) {
+#define DVIE_HB_CASE(N) \
+  case N:               \
+    DVIE_HB_VMCNT(N);   \
+    break;
+    DVIE_HB_CASE(1) DVIE_HB_CASE(2) DVIE_HB_CASE(3) DVIE_HB_CASE(4) DVIE_HB_CASE(5) DVIE_HB_CASE(6) DVIE_HB_CASE(7)
+    DVIE_HB_CASE(8) DVIE_HB_CASE(9) DVIE_HB_CASE(10) DVIE_HB_CASE(11) DVIE_HB_CASE(12) DVIE_HB_CASE(13) DVIE_HB_CASE(14)
+    DVIE_HB_CASE(15) DVIE_HB_CASE(16) DVIE_HB_CASE(17) DVIE_HB_CASE(18) DVIE_HB_CASE(19) DVIE_HB_CASE(20)
+#undef DVIE_HB_CASE
+    default: __builtin_amdgcn_s_waitcnt(0);
+  }
 }
 
 template <int CO>
@@ -187,14 +211,34 @@ __global__ __launch_bounds__(512) void head3_bwd_kernel(const dvie_head3_bwd_des
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc2[j][e] = 0.f;
 
-  if (t_begin < t_end) issue(t_begin, 0);
+  // output-gradient stores: buffer stores every wave issues (out-of-image pixels at an
+  // out-of-range offset, dropped), so the vector-memory count of a tile is fixed
+  const __amdgpu_buffer_rsrc_t rdh =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dh, 0, (int)(npx * p.dh_ld * 2ull), 0x00020000);
+  constexpr int NSTG = C::NSTG, NST = 4;  // stage buffers; dh stores per wave per tile
+  const int np = C::pieces(wave);
+  const int ntl = t_end - t_begin;
+#pragma unroll
+  for (int j = 0; j < NSTG - 1; ++j)
+    if (j < ntl) issue(t_begin + j, j);
   for (int t = t_begin; t < t_end; ++t) {
-    const int sb = (t - t_begin) & 1;
+    const int li = t - t_begin;
+    const int sb = li % NSTG;
     // this tile's DMA (and the weight stores) have landed for every wave, and every wave is
-    // done reading the buffer the next tile streams into
-    __builtin_amdgcn_s_waitcnt(0);
+    // done reading the buffer tile t + NSTG - 1 streams into.  Issued after this tile's
+    // pieces (in order): tiles li + 1 .. li + NSTG - 2 and the stores of tiles li - NSTG + 1 ..
+    // li - 1 (interleaved), which may stay in flight.
+    if (NSTG == 2) {
+      __builtin_amdgcn_s_waitcnt(0);
+    } else {
+      const int later = (li + 1 < ntl ? np : 0) + (li >= 1 ? NST : 0) + (li >= 2 ? NST : 0);
+      if (later == 0)
+        __builtin_amdgcn_s_waitcnt(0);
+      else
+        hb_wait_vmcnt(later);
+    }
     __builtin_amdgcn_s_barrier();
-    if (t + 1 < t_end) issue(t + 1, sb ^ 1);
+    if (t + NSTG - 1 < t_end) issue(t + NSTG - 1, (li + NSTG - 1) % NSTG);
     const char* S = St + sb * C::STAGE;
     const char* Gh = S + C::HT;
     const Tile T = tile_of(t);
@@ -218,17 +262,23 @@ __global__ __launch_bounds__(512) void head3_bwd_kernel(const dvie_head3_bwd_des
     }
 
     // ---- GEMM 2: partial dW over the tile's 256 pixels ----
+    // (slice sl + 1's fragments are read while slice sl's MFMAs run)
+    {
+      bf16x8 fb[2], fa0[2], fa1[2];
+      auto ld2 = [&](int sl, int buf) {
+        const int pa = ((sl >> 2) * C::HWD + 16 * (sl & 3)) * C::GREC;  // slice's first pixel in the halo
+        fb[buf] = hb_tr_pair(S + b2_off + 16 * sl * 128, S + b2_off + (16 * sl + 4) * 128);
+        if (has0) fa0[buf] = hb_tr_pair(Gh + a2_off0 + pa, Gh + a2_off0 + pa + 4 * C::GREC);
+        if (has1) fa1[buf] = hb_tr_pair(Gh + a2_off1 + pa, Gh + a2_off1 + pa + 4 * C::GREC);
+      };
+      ld2(0, 0);
 #pragma unroll
-    for (int sl = 0; sl < 16; ++sl) {
-      const int pa = ((sl >> 2) * C::HWD + 16 * (sl & 3)) * C::GREC;  // slice's first pixel in the halo
-      const bf16x8 bv = hb_tr_pair(S + b2_off + 16 * sl * 128, S + b2_off + (16 * sl + 4) * 128);
-      if (has0) {
-        const bf16x8 av = hb_tr_pair(Gh + a2_off0 + pa, Gh + a2_off0 + pa + 4 * C::GREC);
-        acc2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc2[0], 0, 0, 0);
-      }
-      if (has1) {
-        const bf16x8 av = hb_tr_pair(Gh + a2_off1 + pa, Gh + a2_off1 + pa + 4 * C::GREC);
-        acc2[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc2[1], 0, 0, 0);
+      for (int sl = 0; sl < 16; ++sl) {
+        if (sl + 1 < 16) ld2(sl + 1, (sl + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (has0) acc2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0[sl & 1], fb[sl & 1], acc2[0], 0, 0, 0);
+        if (has1) acc2[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1[sl & 1], fb[sl & 1], acc2[1], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 
@@ -263,12 +313,11 @@ __global__ __launch_bounds__(512) void head3_bwd_kernel(const dvie_head3_bwd_des
             w[2 * e + 1] *= act_dz(__uint_as_float(((uint32_t)hz[e]) & 0xffff0000u), p.dact, p.alpha);
           }
         }
-        if (in) {
-          i32x4 o;
+        i32x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (int)hb_pack(w[2 * e], w[2 * e + 1]);
-          *(i32x4*)((bf16_t*)p.dh + pix * p.dh_ld + cb * 64 + 8 * c8) = o;
-        }
+        for (int e = 0; e < 4; ++e) o[e] = (int)hb_pack(w[2 * e], w[2 * e + 1]);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            o, rdh, in ? (unsigned)((pix * p.dh_ld + cb * 64 + 8 * c8) * 2) : OOB, 0, 0);
       }
     }
   }
@@ -303,7 +352,7 @@ extern "C" int dvie_head3_bwd(const dvie_head3_bwd_desc* d, void* stream) {
   const int ks16 = (d->cout == 8 ? HbCfg<8>::KS : HbCfg<24>::KS) * 16;
   DVIE_CHECK_ARG(d->kpad >= ks16 && d->kpad % 8 == 0, "head3_bwd: kpad %d < %d", d->kpad, ks16);
   const unsigned long long npx = (unsigned long long)d->n * d->hgt * d->wid;
-  DVIE_CHECK_ARG(npx * (unsigned long long)(d->h_ld > d->g_ld ? d->h_ld : d->g_ld) * 2ull < 0xFFFFFF00ull,
+  DVIE_CHECK_ARG(npx * (unsigned long long)std::max(std::max(d->h_ld, d->g_ld), d->dh_ld) * 2ull < 0xFFFFFF00ull,
                  "head3_bwd: maps exceed the 32-bit buffer range");
   const int tiles_x = (d->wid + 63) / 64, tiles_y = (d->hgt + 3) / 4;
   const long long nt = (long long)tiles_x * tiles_y * d->n;
