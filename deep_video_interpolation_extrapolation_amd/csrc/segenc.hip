@@ -84,18 +84,26 @@ __device__ __forceinline__ void se_stage(const char* Wl, int wrows, const char* 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[b][e] = 0.f;
     }
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const i32x4 a = *(const i32x4*)(Wa + s * 32);
+    // (k-step s + 1's fragments are read while step s's MFMAs run)
+    i32x4 fa[2], fb[2][NB];
+    auto ld = [&](int s, int buf) {
+      fa[buf] = *(const i32x4*)(Wa + s * 32);
       int kc = 2 * s + hh;
       kc = kc < KC ? kc : KC - 1;  // zero-weight padding chunk: any finite source
       const int t = kc / CPT, cc = kc - t * CPT;
 #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const i32x4 bv = *(const i32x4*)(B[b] + ((t / 3) * SW + t % 3) * SP + cc * 16);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, bv),
-                                                         acc[b], 0, 0, 0);
-      }
+      for (int b = 0; b < NB; ++b) fb[buf][b] = *(const i32x4*)(B[b] + ((t / 3) * SW + t % 3) * SP + cc * 16);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + 1 < KS) ld(s + 1, (s + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fa[s & 1]),
+                                                         __builtin_bit_cast(bf16x8, fb[s & 1][b]), acc[b], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
