@@ -33,7 +33,7 @@ KIND_NAMES = {2: "conv_wgrad", 3: "wgrad_reduce", 4: "bias_colsum", 5: "pointwis
 # HBM bytes per launch of the conv fwd+dgrad family from PMC counters (tools/pmc_bench.sh on
 # this same bench command; FETCH_SIZE x2 gfx950 correction), committed under profiles/
 # per workload; None: no PMC pass on this workload -> "traffic": null
-PMC_DIRS = {"c2": "r06pmc/pmc", "c5": None}
+PMC_DIRS = {"c2": "r06final/pmc", "c5": None}
 
 
 
