@@ -25,7 +25,7 @@ void set_error(const char* fmt, ...);
     }                                  \
   } while (0)
 
-// Timing-only ablation switches (DVIE_1X1_DBG / DVIE_HALO_DBG / DVIE_NARROW_DBG skip stores,
+// Timing-only ablation switches (DVIE_1X1_DBG / DVIE_HALO_DBG / DVIE_NARROW_DBG / DVIE_SEGENC_DBG skip stores,
 // MFMAs or operand streams, so results are wrong) exist only in a build made with
 // -DDVIE_TIMING_DBG; in the product build the kernels see a constant 0 and the host never
 // reads those variables.

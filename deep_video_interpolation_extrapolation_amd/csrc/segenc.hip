@@ -443,6 +443,7 @@ __global__ __launch_bounds__(512) void segenc_bwd_kernel(const dvie_segenc_bwd_d
                                                          int n_tiles, int dbg) {
   typedef SbCfg C;
   constexpr int NW = C::NW;
+  dbg = DVIE_DBG(dbg);  // (timing-only ablations: a constant 0 outside -DDVIE_TIMING_DBG builds)
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -746,8 +747,11 @@ extern "C" int dvie_segenc_bwd(const dvie_segenc_bwd_desc* d, void* stream) {
   const int tiles_x = (d->w + 63) / 64, tiles_y = (d->h + 3) / 4;
   const long long nt = (long long)tiles_x * tiles_y * d->n;
   DVIE_CHECK_ARG(nt < (1LL << 30), "segenc_bwd: too many tiles");
-  const char* dbg = getenv("DVIE_SEGENC_DBG");  // timing-only ablations (tools/segenc_micro.py)
+  int dbg = 0;  // DVIE_SEGENC_DBG: timing-only ablations (tools/segenc_micro.py), -DDVIE_TIMING_DBG builds only
+#ifdef DVIE_TIMING_DBG
+  if (const char* e = getenv("DVIE_SEGENC_DBG")) dbg = atoi(e);
+#endif
   DVIE_LAUNCH(segenc_bwd_kernel, dim3(d->slabs), dim3(512), 0, (hipStream_t)stream, *d, tiles_x, tiles_y,
-                     (int)nt, dbg && *dbg ? atoi(dbg) : 0);
+                     (int)nt, dbg);
   DVIE_RETURN_LAUNCH();
 }

@@ -2,7 +2,9 @@
 the bench shape, 8 x 256 x 512, synthetic bf16 maps), timed with HIP events per launch, under
 each value of DVIE_SEGENC_DBG given on the command line (timing-only phase ablations read per
 launch: 1 / 2 / 4 skip phase 1 / 2 / 3, 8 the tile loads, 16 the slab stores, 32 the tile loop;
-0 = the real kernel).
+0 = the real kernel).  The ablation bits exist only in the timing-only library
+(-DDVIE_TIMING_DBG, results wrong; the product build ignores DVIE_SEGENC_DBG): copy that build
+over the package's libdvie.so first, as tools/skip_ab.sh does.
 usage: python tools/segenc_micro.py [dbg values ...]"""
 import ctypes
 import os
